@@ -1,0 +1,216 @@
+"""MI355X beam-radiance-estimate gather — Python bindings over the C ABI of libbre.so.
+
+The product is the C ABI in ``include/bre.h`` (libbre.so, hand-written HIP for gfx950).  This
+module is a thin ctypes binding used by the tests, ``bench.py`` and ``__graft_entry__``; it has
+no compute of its own and no CPU fallback: if libbre.so is missing or no GPU is present, the
+calls fail loudly.
+
+Import with ``importlib.import_module("beam-radiance-estimate-pbrt_amd")`` (the directory name
+is not a Python identifier) or via ``tests/conftest.py``'s ``bre`` fixture.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbre.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "bre.h")
+
+BRE_OK = 0
+STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE_ERR_OOM",
+                4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
+OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE = 1, 2, 3, 4, 5
+
+# Every entry point include/bre.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "bre_abi_version", "bre_create", "bre_destroy", "bre_last_error", "bre_set_option",
+    "bre_set_stream", "bre_synchronize", "bre_get_stats", "bre_set_beams",
+    "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
+    "bre_resolve_image",
+]
+
+
+class BreError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_beams", ctypes.c_int64), ("n_beams_valid", ctypes.c_int64),
+                ("n_nodes", ctypes.c_int64), ("n_segments", ctypes.c_int64),
+                ("candidates", ctypes.c_int64), ("contributions", ctypes.c_int64),
+                ("node_visits", ctypes.c_int64), ("build_ms", ctypes.c_double),
+                ("gather_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libbre.so and declare its signatures.  Raises if it is not built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    # PyTorch-ROCm bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever is
+    # loaded first serves the whole process, and torch cannot initialise on a runtime it was not
+    # built with, so load torch's first whenever torch is installed (it is the process's
+    # allocator / stream / RCCL plumbing in bench.py and the device-pointer tests).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not found: build it with `make -C {HERE}/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    P, I64, I32, F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+    lib.bre_abi_version.restype = I32
+    lib.bre_create.argtypes = [I32, ctypes.POINTER(P)]
+    lib.bre_create.restype = I32
+    lib.bre_destroy.argtypes = [P]
+    lib.bre_destroy.restype = None
+    lib.bre_last_error.argtypes = [P]
+    lib.bre_last_error.restype = ctypes.c_char_p
+    lib.bre_set_option.argtypes = [P, I32, I64]
+    lib.bre_set_option.restype = I32
+    lib.bre_set_stream.argtypes = [P, P]
+    lib.bre_set_stream.restype = I32
+    lib.bre_synchronize.argtypes = [P]
+    lib.bre_synchronize.restype = I32
+    lib.bre_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+    lib.bre_get_stats.restype = I32
+    for fn in (lib.bre_set_beams, lib.bre_set_beams_device):
+        fn.argtypes = [P, I64, P, P, P, P]
+        fn.restype = I32
+    for fn in (lib.bre_gather, lib.bre_gather_device):
+        fn.argtypes = [P, I64, P, P, P, P, P, F, I64, P, P, P]
+        fn.restype = I32
+    lib.bre_beam_radius_at.argtypes = [F, F, I32]
+    lib.bre_beam_radius_at.restype = F
+    lib.bre_resolve_image.argtypes = [I64, P, I32, P]
+    lib.bre_resolve_image.restype = I32
+    _LIB = lib
+    return lib
+
+
+def _ptr(a):
+    """Raw pointer of a numpy array or a torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor
+
+
+def _f32(a, n3=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a
+
+
+class BeamGather:
+    """One libbre context on one GPU (mirrors the life of one PhotonBeamBVH + gather loop)."""
+
+    def __init__(self, device: int = 0, counters: bool = False, timing: bool = False, kernel: int = 0,
+                 leaf_size: int | None = None, sqrt_mode: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        st = self.lib.bre_create(device, ctypes.byref(h))
+        if st != BRE_OK:
+            raise BreError(st, f"bre_create(device={device}) failed")
+        self.h = h
+        self.set_option(OPT_COUNTERS, int(counters))
+        self.set_option(OPT_TIMING, int(timing))
+        self.set_option(OPT_KERNEL, kernel)
+        self.set_option(OPT_SQRT_MODE, sqrt_mode)
+        if leaf_size is not None:
+            self.set_option(OPT_LEAF_SIZE, leaf_size)
+        self._keep = []
+
+    def _check(self, st):
+        if st != BRE_OK:
+            raise BreError(st, self.lib.bre_last_error(self.h).decode())
+
+    def set_option(self, opt: int, value: int):
+        self._check(self.lib.bre_set_option(self.h, opt, int(value)))
+
+    def set_stream(self, stream_handle: int | None):
+        self._check(self.lib.bre_set_stream(self.h, stream_handle))
+
+    def synchronize(self):
+        self._check(self.lib.bre_synchronize(self.h))
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._check(self.lib.bre_get_stats(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    # ---- beams ----
+    def set_beams(self, start, end, radius, power):
+        """Host arrays (numpy): copies to the GPU and builds the BVH."""
+        start, end, radius, power = (_f32(x) for x in (start, end, radius, power))
+        n = radius.shape[0]
+        assert start.shape == (n, 3) and end.shape == (n, 3) and power.shape == (n, 3)
+        self._check(self.lib.bre_set_beams(self.h, n, _ptr(start), _ptr(end), _ptr(radius), _ptr(power)))
+
+    def set_beams_device(self, start, end, radius, power):
+        """Device tensors (torch, float32, contiguous)."""
+        n = radius.shape[0]
+        for t in (start, end, radius, power):
+            assert t.is_cuda and t.is_contiguous() and str(t.dtype) == "torch.float32"
+        self._keep = [start, end, radius, power]
+        self._check(self.lib.bre_set_beams_device(self.h, n, _ptr(start), _ptr(end), _ptr(radius), _ptr(power)))
+
+    # ---- gather ----
+    def gather(self, o, p, d, tmax, pixel=None, R=0.01, npix=0, accum=None, seg_rgb=True, counts=False):
+        """Host arrays.  Returns dict with 'seg_rgb' (nseg,3) and optionally 'counts' (nseg,2);
+        `accum` (npix,3) float32 is updated in place when given."""
+        o, p, d, tmax = (_f32(x) for x in (o, p, d, tmax))
+        n = tmax.shape[0]
+        pix = None if pixel is None else np.ascontiguousarray(pixel, dtype=np.int32)
+        out = np.zeros((n, 3), np.float32) if seg_rgb else None
+        cnt = np.zeros((n, 2), np.int32) if counts else None
+        if accum is not None:
+            assert accum.dtype == np.float32 and accum.flags.c_contiguous
+        self._check(self.lib.bre_gather(self.h, n, _ptr(o), _ptr(p), _ptr(d), _ptr(tmax), _ptr(pix), float(R),
+                                        int(npix), _ptr(accum), _ptr(out), _ptr(cnt)))
+        res = {}
+        if out is not None:
+            res["seg_rgb"] = out
+        if cnt is not None:
+            res["counts"] = cnt
+        return res
+
+    def gather_device(self, o, p, d, tmax, pixel, R, npix, accum=None, seg_rgb=None, counts=None):
+        """Device tensors; asynchronous on the context stream."""
+        n = tmax.shape[0]
+        self._check(self.lib.bre_gather_device(self.h, n, _ptr(o), _ptr(p), _ptr(d), _ptr(tmax), _ptr(pixel),
+                                               float(R), int(npix), _ptr(accum), _ptr(seg_rgb), _ptr(counts)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.bre_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def beam_radius_at(initial_radius: float, alpha: float, iteration: int) -> float:
+    """currentBeamRadius at `iteration` (photonbeam.cpp:354-356, 562), via libbre."""
+    return float(load_library().bre_beam_radius_at(initial_radius, alpha, iteration))

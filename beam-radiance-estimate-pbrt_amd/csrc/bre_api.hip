@@ -1,0 +1,445 @@
+// bre_api.hip — C ABI of libbre.so (include/bre.h): context, device memory, build and gather
+// orchestration on one HIP stream.  No exceptions cross the ABI; every failure is a status code
+// plus a message for bre_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bre.h"
+#include "bre_device.h"
+
+using namespace bre;
+
+namespace {
+
+struct DevMem {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&ptr, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T *as() const {
+        return static_cast<T *>(ptr);
+    }
+};
+
+}  // namespace
+
+struct bre_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    // options
+    bool counters = false;
+    bool timing = false;
+    int kernel = 0;
+    int leaf_size = 4;
+    int sqrt_mode = 0;
+    // beam set
+    int64_t nbeams = 0, nvalid = 0, nnodes = 0;
+    int built_leaf_size = 4;
+    DevMem in_start, in_end, in_radius, in_power;  // staging for host-pointer uploads
+    DevMem box, cent, cbounds, nvalid_buf, keys, keys_alt, vals, vals_alt, sort_tmp, leaf_parent, visit;
+    DevMem recs, pow, nodes;
+    // gather staging (host-pointer API)
+    DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
+    DevMem counters_buf;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bre_stats stats;
+};
+
+namespace {
+
+bre_status fail(bre_ctx *c, bre_status st, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return st;
+}
+
+#define HIPCHK(ctx, call)                                                                                    \
+    do {                                                                                                     \
+        hipError_t e_ = (call);                                                                              \
+        if (e_ != hipSuccess)                                                                                \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? BRE_ERR_OOM : BRE_ERR_HIP, "%s: %s (%s:%d)", #call, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                                          \
+    } while (0)
+
+bre_status set_device(bre_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    return BRE_OK;
+}
+
+// Build the BVH from device arrays (start/end/radius/power) of n beams.
+bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, const float *radius,
+                 const float *power) {
+    c->nbeams = n;
+    c->nvalid = 0;
+    c->nnodes = 0;
+    c->stats = bre_stats{};
+    c->stats.n_beams = n;
+    if (n == 0) return BRE_OK;
+    if (n > (int64_t)INT32_MAX / 2)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams: %lld beams exceeds the 2^30 limit of this build",
+                    (long long)n);
+    const size_t N = (size_t)n;
+    HIPCHK(c, c->box.ensure(N * 6 * sizeof(float)));
+    HIPCHK(c, c->cent.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->cbounds.ensure(6 * sizeof(unsigned int)));
+    HIPCHK(c, c->nvalid_buf.ensure(sizeof(unsigned int)));
+    HIPCHK(c, c->keys.ensure(N * sizeof(unsigned long long)));
+    HIPCHK(c, c->keys_alt.ensure(N * sizeof(unsigned long long)));
+    HIPCHK(c, c->vals.ensure(N * sizeof(int32_t)));
+    HIPCHK(c, c->vals_alt.ensure(N * sizeof(int32_t)));
+    const size_t tmp = sort_temp_bytes(n);
+    HIPCHK(c, c->sort_tmp.ensure(tmp));
+    BuildBuffers b;
+    b.start = start;
+    b.end = end;
+    b.radius = radius;
+    b.power = power;
+    b.n = n;
+    b.sqrt_mode = c->sqrt_mode;
+    b.leaf_size = c->leaf_size;
+    b.box = c->box.as<float>();
+    b.cent = c->cent.as<float>();
+    b.cbounds = c->cbounds.as<unsigned int>();
+    b.nvalid = c->nvalid_buf.as<unsigned int>();
+    b.keys = c->keys.as<unsigned long long>();
+    b.keys_alt = c->keys_alt.as<unsigned long long>();
+    b.vals = c->vals.as<int32_t>();
+    b.vals_alt = c->vals_alt.as<int32_t>();
+    b.sort_tmp = c->sort_tmp.ptr;
+    b.sort_tmp_bytes = c->sort_tmp.cap;
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, launch_prep(b, c->stream));
+    HIPCHK(c, launch_morton(b, c->stream));
+    HIPCHK(c, launch_sort(b, c->stream));
+    unsigned int nv = 0;
+    HIPCHK(c, hipMemcpyAsync(&nv, b.nvalid, sizeof(nv), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t nvalid = nv;
+    c->nvalid = nvalid;
+    c->stats.n_beams_valid = nvalid;
+    if (nvalid == 0) return BRE_OK;
+    const int K = c->leaf_size;
+    const int64_t nleaf = (nvalid + K - 1) / K;
+    const int64_t nnodes = nleaf > 1 ? nleaf - 1 : 1;
+    HIPCHK(c, c->recs.ensure((size_t)nvalid * sizeof(BeamRec)));
+    HIPCHK(c, c->pow.ensure((size_t)nvalid * sizeof(float4)));
+    HIPCHK(c, c->nodes.ensure((size_t)nnodes * sizeof(Node)));
+    HIPCHK(c, c->leaf_parent.ensure((size_t)nleaf * sizeof(int32_t)));
+    HIPCHK(c, c->visit.ensure((size_t)nnodes * sizeof(unsigned int)));
+    b.recs = c->recs.as<BeamRec>();
+    b.pow = c->pow.as<float4>();
+    b.nodes = c->nodes.as<Node>();
+    b.leaf_parent = c->leaf_parent.as<int32_t>();
+    b.visit = c->visit.as<unsigned int>();
+    HIPCHK(c, launch_pack(b, nvalid, c->stream));
+    HIPCHK(c, launch_hierarchy(b, nvalid, c->stream));
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev[1]));
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->stats.build_ms = ms;
+    }
+    c->nnodes = nnodes;
+    c->built_leaf_size = K;
+    c->stats.n_nodes = nnodes;
+    return BRE_OK;
+}
+
+bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
+                         const int32_t *pixel, float R, int64_t npix, float *accum, float *seg_rgb,
+                         int32_t *seg_counts) {
+    if (nseg < 0 || npix < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: negative size");
+    if (nseg > 0 && (!o || !p || !d || !tmax))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: null segment array");
+    if (accum && !pixel) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: accum_rgb given without seg_pixel");
+    if (seg_counts && !c->counters)
+        return fail(c, BRE_ERR_STATE, "bre_gather: seg_counts needs BRE_OPT_COUNTERS=1");
+    HIPCHK(c, c->counters_buf.ensure(sizeof(DevCounters)));
+    DevCounters *ctr = c->counters_buf.as<DevCounters>();
+    HIPCHK(c, hipMemsetAsync(ctr, 0, sizeof(DevCounters), c->stream));
+    GatherArgs a;
+    a.nseg = nseg;
+    a.o = o;
+    a.p = p;
+    a.d = d;
+    a.tmax = tmax;
+    a.pixel = pixel;
+    a.R = R;
+    a.npix = npix;
+    a.accum = accum;
+    a.seg_rgb = seg_rgb;
+    a.seg_counts = seg_counts;
+    a.recs = c->recs.as<BeamRec>();
+    a.pow = c->pow.as<float4>();
+    a.nodes = c->nodes.as<Node>();
+    a.nvalid = c->nvalid;
+    a.leaf_size = c->built_leaf_size;
+    a.ctr = ctr;
+    c->stats.n_segments = nseg;
+    if (c->nvalid == 0) {
+        // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
+        HIPCHK(c, launch_zero_outputs(a, c->stream));
+        return BRE_OK;
+    }
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(c, launch_gather(a, c->kernel == 2 ? 2 : 1, c->counters, c->stream));
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+    if (c->timing || c->counters) {
+        DevCounters h;
+        HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->timing) {
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+            c->stats.gather_ms = ms;
+        }
+        c->stats.candidates = (int64_t)h.candidates;
+        c->stats.contributions = (int64_t)h.contributions;
+        c->stats.node_visits = (int64_t)h.node_visits;
+        if (h.flags & 1u) return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than stack)");
+        if (h.flags & 2u) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix)");
+    }
+    return BRE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bre_abi_version(void) { return BRE_ABI_VERSION; }
+
+bre_status bre_create(int device, bre_ctx **out) {
+    if (!out) return BRE_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BRE_ERR_NO_DEVICE;
+    if (device < 0 || device >= count) return BRE_ERR_NO_DEVICE;
+    bre_ctx *c = new bre_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return BRE_ERR_HIP;
+    }
+    c->own_stream = true;
+    for (auto &e : c->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete c;
+            return BRE_ERR_HIP;
+        }
+    }
+    *out = c;
+    return BRE_OK;
+}
+
+void bre_destroy(bre_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevMem *all[] = {&c->in_start, &c->in_end, &c->in_radius, &c->in_power, &c->box,      &c->cent,
+                     &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
+                     &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
+                     &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf};
+    for (DevMem *m : all) m->release();
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *bre_last_error(const bre_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    switch (option) {
+    case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
+    case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
+    case BRE_OPT_KERNEL:
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0, 1 or 2");
+        c->kernel = (int)value;
+        return BRE_OK;
+    case BRE_OPT_LEAF_SIZE:
+        if (value < 1 || value > 16) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_LEAF_SIZE must be in 1..16");
+        c->leaf_size = (int)value;
+        return BRE_OK;
+    case BRE_OPT_SQRT_MODE:
+        if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SQRT_MODE must be 0 or 1");
+        c->sqrt_mode = (int)value;
+        return BRE_OK;
+    default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
+    }
+}
+
+bre_status bre_set_stream(bre_ctx *c, void *stream) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (c->own_stream && c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+        c->own_stream = false;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+            return fail(c, BRE_ERR_HIP, "hipStreamCreate failed");
+        c->own_stream = true;
+    }
+    return BRE_OK;
+}
+
+bre_status bre_synchronize(bre_ctx *c) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
+bre_status bre_get_stats(const bre_ctx *c, bre_stats *out) {
+    if (!c || !out) return BRE_ERR_INVALID_ARG;
+    *out = c->stats;
+    return BRE_OK;
+}
+
+bre_status bre_set_beams(bre_ctx *c, int64_t n, const float *start, const float *end, const float *radius,
+                         const float *power) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (n < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams: negative count");
+    if (n > 0 && (!start || !end || !radius || !power))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams: null array");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    const size_t N = (size_t)n;
+    if (n > 0) {
+        HIPCHK(c, c->in_start.ensure(N * 3 * sizeof(float)));
+        HIPCHK(c, c->in_end.ensure(N * 3 * sizeof(float)));
+        HIPCHK(c, c->in_radius.ensure(N * sizeof(float)));
+        HIPCHK(c, c->in_power.ensure(N * 3 * sizeof(float)));
+        HIPCHK(c, hipMemcpyAsync(c->in_start.ptr, start, N * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->in_end.ptr, end, N * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->in_radius.ptr, radius, N * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->in_power.ptr, power, N * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    }
+    st = build(c, n, c->in_start.as<float>(), c->in_end.as<float>(), c->in_radius.as<float>(),
+               c->in_power.as<float>());
+    if (st != BRE_OK) return st;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
+bre_status bre_set_beams_device(bre_ctx *c, int64_t n, const float *start, const float *end, const float *radius,
+                                const float *power) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (n < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams_device: negative count");
+    if (n > 0 && (!start || !end || !radius || !power))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams_device: null array");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    return build(c, n, start, end, radius, power);
+}
+
+bre_status bre_gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d,
+                             const float *tmax, const int32_t *pixel, float R, int64_t npix, float *accum,
+                             float *seg_rgb, int32_t *seg_counts) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    return gather_device(c, nseg, o, p, d, tmax, pixel, R, npix, accum, seg_rgb, seg_counts);
+}
+
+bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
+                      const int32_t *pixel, float R, int64_t npix, float *accum, float *seg_rgb,
+                      int32_t *seg_counts) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (nseg < 0 || npix < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: negative size");
+    if (nseg > 0 && (!o || !p || !d || !tmax))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: null segment array");
+    if (accum && !pixel) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: accum_rgb given without seg_pixel");
+    if (accum && pixel) {
+        for (int64_t s = 0; s < nseg; ++s)
+            if (pixel[s] < 0 || pixel[s] >= npix)
+                return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel[%lld]=%d out of [0,%lld)", (long long)s,
+                            pixel[s], (long long)npix);
+    }
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    const size_t S = (size_t)nseg, P = (size_t)npix;
+    if (nseg == 0) return BRE_OK;
+    HIPCHK(c, c->g_o.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->g_p.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->g_d.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->g_tmax.ensure(S * sizeof(float)));
+    HIPCHK(c, hipMemcpyAsync(c->g_o.ptr, o, S * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->g_p.ptr, p, S * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->g_d.ptr, d, S * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->g_tmax.ptr, tmax, S * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    int32_t *dpix = nullptr;
+    float *daccum = nullptr, *dseg = nullptr;
+    int32_t *dcnt = nullptr;
+    if (pixel) {
+        HIPCHK(c, c->g_pix.ensure(S * sizeof(int32_t)));
+        HIPCHK(c, hipMemcpyAsync(c->g_pix.ptr, pixel, S * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        dpix = c->g_pix.as<int32_t>();
+    }
+    if (accum && npix > 0) {
+        HIPCHK(c, c->g_accum.ensure(P * 3 * sizeof(float)));
+        HIPCHK(c, hipMemcpyAsync(c->g_accum.ptr, accum, P * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        daccum = c->g_accum.as<float>();
+    }
+    if (seg_rgb) {
+        HIPCHK(c, c->g_seg_rgb.ensure(S * 3 * sizeof(float)));
+        dseg = c->g_seg_rgb.as<float>();
+    }
+    if (seg_counts) {
+        HIPCHK(c, c->g_counts.ensure(S * 2 * sizeof(int32_t)));
+        dcnt = c->g_counts.as<int32_t>();
+    }
+    st = gather_device(c, nseg, c->g_o.as<float>(), c->g_p.as<float>(), c->g_d.as<float>(), c->g_tmax.as<float>(), dpix,
+                       R, npix, daccum, dseg, dcnt);
+    if (st != BRE_OK) return st;
+    if (daccum) HIPCHK(c, hipMemcpyAsync(accum, daccum, P * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    if (dseg) HIPCHK(c, hipMemcpyAsync(seg_rgb, dseg, S * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    if (dcnt) HIPCHK(c, hipMemcpyAsync(seg_counts, dcnt, S * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
+float bre_beam_radius_at(float initial_radius, float alpha, int iteration) {
+    float r = initial_radius;
+    for (int i = 0; i < iteration; ++i) r = r * (float(i + alpha) / float(i + 1));
+    return r;
+}
+
+bre_status bre_resolve_image(int64_t npix, const float *ld, int iteration, float *out) {
+    if (npix < 0 || (npix > 0 && (!ld || !out)) || iteration < 0) return BRE_ERR_INVALID_ARG;
+    // Spectrum L = pixel.Ld / (iter + 1): operator/(Float) divides each channel (spectrum.h:180-186)
+    const float div = (float)(iteration + 1);
+    for (int64_t i = 0; i < 3 * npix; ++i) out[i] = ld[i] / div;
+    return BRE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,382 @@
+// bre_build.hip — GPU build of the beam BVH for gfx950.
+//
+// Replaces the reference's single-threaded SAH build (PhotonBeamBVH ctor + recursiveBuild +
+// flattenBVH2Tree, src/core/photonbeambvh.cpp:204-248, 259-425, 663-681) with a Karras-style
+// linear BVH over 63-bit Morton codes of the beam-box centroids — the GPU form of the
+// reference's own (unused) HLBVH path (EncodeMorton3 / RadixSort / emitLBVH2, :109-182, 427-559).
+//
+// The tree shape does not have to match the reference: the set of beams gathered for a
+// segment is the set whose *own test box* passes Bounds3::IntersectP (see DESIGN.md "key
+// enabler").  The one place where the reference's tree leaks into that set is a leaf holding
+// several beams, which recursiveBuild creates exactly for beams with bit-identical centroids
+// (:289-297); their leaf box (the union) is what the reference tests.  k_pack reproduces that by
+// giving every beam the union box of its equal-centroid group.
+//
+// Passes (all on the context stream):
+//   k_prep      per beam: WorldBound box (reference arithmetic), centroid, validity, centroid bounds
+//   k_morton    per beam: 63-bit Morton key of the centroid (invalid beams sort last)
+//   radix sort  rocPRIM radix_sort_pairs (key, beam index)
+//   k_pack      per sorted beam: equal-centroid group box, 64-B BeamRec, scaled power
+//   k_karras    per interior node: Karras 2012 split over leaf clusters of `leaf_size` beams
+//   k_refit     per leaf cluster: bottom-up union of child boxes (agent-scope release/acquire
+//               hand-off through one counter per node, cdna_hip_programming.md Guideline 16)
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <float.h>
+
+#include "bre_device.h"
+#include "bre_math.h"
+
+namespace bre {
+
+namespace {
+
+__device__ __forceinline__ unsigned int f2ord(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ bool finite6(const float *b) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ok = ok && isfinite(b[k]);
+    return ok;
+}
+
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start, const float *__restrict__ end,
+                                                 const float *__restrict__ radius, int64_t n, int sqrt_mode,
+                                                 float *__restrict__ box, float *__restrict__ cent,
+                                                 unsigned int *__restrict__ cbounds, unsigned int *__restrict__ nvalid) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    // ordered-uint min (lo) / max (hi) of valid centroids; identity values
+    unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
+    unsigned int mx[3] = {0u, 0u, 0u};
+    bool valid = false;
+    if (i < n) {
+        const f3 s = mk(start[3 * i], start[3 * i + 1], start[3 * i + 2]);
+        const f3 e = mk(end[3 * i], end[3 * i + 1], end[3 * i + 2]);
+        f3 lo, hi;
+        world_bound(s, e, radius[i], sqrt_mode, lo, hi);
+        float b[6] = {lo.x, lo.y, lo.z, hi.x, hi.y, hi.z};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) box[6 * i + k] = b[k];
+        // centroid = .5f * pMin + .5f * pMax  (photonbeambvh.cpp:51-54)
+        const f3 c = add3(scale3(lo, .5f), scale3(hi, .5f));
+        cent[3 * i] = c.x;
+        cent[3 * i + 1] = c.y;
+        cent[3 * i + 2] = c.z;
+        valid = finite6(b) && isfinite(c.x) && isfinite(c.y) && isfinite(c.z);
+        if (valid) {
+            mn[0] = mx[0] = f2ord(c.x);
+            mn[1] = mx[1] = f2ord(c.y);
+            mn[2] = mx[2] = f2ord(c.z);
+        }
+    }
+    // wave reduction (64 lanes) then one atomic per wave
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], off));
+            mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
+        }
+    }
+    const unsigned long long vm = __ballot(valid);
+    if ((threadIdx.x & 63) == 0 && vm != 0ull) {
+        atomicAdd(nvalid, (unsigned int)__popcll(vm));
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(&cbounds[k], mn[k]);
+            atomicMax(&cbounds[3 + k], mx[k]);
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned long long expand21(unsigned int v) {
+    unsigned long long x = v & 0x1fffffull;
+    x = (x | (x << 32)) & 0x1f00000000ffffull;
+    x = (x | (x << 16)) & 0x1f0000ff0000ffull;
+    x = (x | (x << 8)) & 0x100f00f00f00f00full;
+    x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+    x = (x | (x << 2)) & 0x1249249249249249ull;
+    return x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_morton(const float *__restrict__ box, const float *__restrict__ cent,
+                                                   const unsigned int *__restrict__ cbounds, int64_t n,
+                                                   unsigned long long *__restrict__ keys, int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float b[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = box[6 * i + k];
+    const float c[3] = {cent[3 * i], cent[3 * i + 1], cent[3 * i + 2]};
+    unsigned long long key = ~0ull;
+    if (finite6(b) && isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2])) {
+        unsigned int q[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float lo = ord2f(cbounds[k]), hi = ord2f(cbounds[3 + k]);
+            const float ext = hi - lo;
+            float u = ext > 0.0f ? (c[k] - lo) / ext : 0.0f;
+            u = fminf(fmaxf(u * 2097152.0f, 0.0f), 2097151.0f);
+            q[k] = (unsigned int)u;
+        }
+        key = (expand21(q[2]) << 2) | (expand21(q[1]) << 1) | expand21(q[0]);
+    }
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start, const float *__restrict__ end,
+                                                 const float *__restrict__ radius, const float *__restrict__ power,
+                                                 const float *__restrict__ box, const float *__restrict__ cent,
+                                                 const unsigned long long *__restrict__ keys,
+                                                 const int32_t *__restrict__ vals, int64_t nvalid,
+                                                 BeamRec *__restrict__ recs, float4 *__restrict__ pw) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= nvalid) return;
+    const int32_t i = vals[s];
+    const unsigned long long key = keys[s];
+    float lo[3] = {box[6 * i], box[6 * i + 1], box[6 * i + 2]};
+    float hi[3] = {box[6 * i + 3], box[6 * i + 4], box[6 * i + 5]};
+    const float c0 = cent[3 * i], c1 = cent[3 * i + 1], c2 = cent[3 * i + 2];
+    // Equal-centroid group (the reference's multi-beam SAH leaf): union of the members' boxes.
+    // Members share the Morton key, so they are within this key run.
+    for (int64_t t = s - 1; t >= 0 && keys[t] == key; --t) {
+        const int32_t j = vals[t];
+        if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = smin(lo[k], box[6 * j + k]);
+                hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+            }
+        }
+    }
+    for (int64_t t = s + 1; t < nvalid && keys[t] == key; ++t) {
+        const int32_t j = vals[t];
+        if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = smin(lo[k], box[6 * j + k]);
+                hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+            }
+        }
+    }
+    const f3 b0 = mk(start[3 * i], start[3 * i + 1], start[3 * i + 2]);
+    const f3 b1 = mk(end[3 * i], end[3 * i + 1], end[3 * i + 2]);
+    const f3 B = sub3(b1, b0);
+    const float magB = len3(B);
+    const f3 bu = div3(B, magB);
+    BeamRec r;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = lo[k];
+        r.hi[k] = hi[k];
+    }
+    r.b0[0] = b0.x; r.b0[1] = b0.y; r.b0[2] = b0.z;
+    r.bu[0] = bu.x; r.bu[1] = bu.y; r.bu[2] = bu.z;
+    r.mag_b = magB;
+    r.radius = radius[i];
+    r.pad[0] = 0.0f;
+    r.pad[1] = 0.0f;
+    recs[s] = r;
+    // `1e-5 * beam->powerEnd` = powerEnd.c[k] * (Float)1e-5  (photonbeam.cpp:504, spectrum.h:165-179)
+    const float k5 = 1e-5f;
+    pw[s] = make_float4(power[3 * i] * k5, power[3 * i + 1] * k5, power[3 * i + 2] * k5, 0.0f);
+}
+
+__device__ __forceinline__ int ldelta(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf, int i, int j) {
+    if (j < 0 || j >= nleaf) return -1;
+    const unsigned long long ki = keys[(int64_t)i * leaf_size], kj = keys[(int64_t)j * leaf_size];
+    if (ki == kj) return 64 + __clz((unsigned int)(i ^ j));
+    return __clzll(ki ^ kj);
+}
+
+__global__ __launch_bounds__(kBlock) void k_karras(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf,
+                                                   Node *__restrict__ nodes, int32_t *__restrict__ leaf_parent) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nleaf - 1) return;
+    const int d = (ldelta(keys, leaf_size, nleaf, i, i + 1) - ldelta(keys, leaf_size, nleaf, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = ldelta(keys, leaf_size, nleaf, i, i - d);
+    int lmax = 2;
+    while (ldelta(keys, leaf_size, nleaf, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (ldelta(keys, leaf_size, nleaf, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = ldelta(keys, leaf_size, nleaf, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (ldelta(keys, leaf_size, nleaf, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + min(d, 0);
+    const int lo = min(i, j), hi = max(i, j);
+    int32_t left, right;
+    if (lo == gamma) {
+        left = ~gamma;
+        leaf_parent[gamma] = i;
+    } else {
+        left = gamma;
+        nodes[gamma].parent = i;
+    }
+    if (hi == gamma + 1) {
+        right = ~(gamma + 1);
+        leaf_parent[gamma + 1] = i;
+    } else {
+        right = gamma + 1;
+        nodes[gamma + 1].parent = i;
+    }
+    nodes[i].child[0] = left;
+    nodes[i].child[1] = right;
+    nodes[i].pad = 0;
+    if (i == 0) nodes[0].parent = -1;
+}
+
+__device__ __forceinline__ void leaf_box(const BeamRec *__restrict__ recs, int64_t nvalid, int leaf_size, int c,
+                                         float lo[3], float hi[3]) {
+    const int64_t first = (int64_t)c * leaf_size;
+    const int64_t last = min(first + leaf_size, nvalid);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = FLT_MAX;
+        hi[k] = -FLT_MAX;
+    }
+    for (int64_t b = first; b < last; ++b) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fminf(lo[k], recs[b].lo[k]);
+            hi[k] = fmaxf(hi[k], recs[b].hi[k]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_refit(const BeamRec *__restrict__ recs, int64_t nvalid, int leaf_size,
+                                                  int nleaf, Node *nodes, const int32_t *__restrict__ leaf_parent,
+                                                  unsigned int *visit) {
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= nleaf) return;
+    float lo[3], hi[3];
+    leaf_box(recs, nvalid, leaf_size, c, lo, hi);
+    int32_t me = ~c;
+    int32_t p = leaf_parent[c];
+    while (p >= 0) {
+        const int slot = (nodes[p].child[0] == me) ? 0 : 1;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            nodes[p].lo[slot][k] = lo[k];
+            nodes[p].hi[slot][k] = hi[k];
+        }
+        // release our slot, then count arrivals at p (Guideline 16: release -> vmcnt(0) -> atomic)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int old = __hip_atomic_fetch_add(&visit[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 0u) return;  // sibling not done yet; it will carry p upward
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float a = __hip_atomic_load(&nodes[p].lo[0][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float b = __hip_atomic_load(&nodes[p].lo[1][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float e = __hip_atomic_load(&nodes[p].hi[0][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float f = __hip_atomic_load(&nodes[p].hi[1][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lo[k] = fminf(a, b);
+            hi[k] = fmaxf(e, f);
+        }
+        me = p;
+        p = nodes[p].parent;
+    }
+}
+
+// Single-leaf tree: one root whose second child is empty.
+__global__ void k_single(const BeamRec *__restrict__ recs, int64_t nvalid, int leaf_size, Node *nodes) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float lo[3], hi[3];
+    leaf_box(recs, nvalid, leaf_size, 0, lo, hi);
+    Node n;
+    for (int k = 0; k < 3; ++k) {
+        n.lo[0][k] = lo[k];
+        n.hi[0][k] = hi[k];
+        n.lo[1][k] = FLT_MAX;
+        n.hi[1][k] = -FLT_MAX;
+    }
+    n.child[0] = ~0;
+    n.child[1] = kEmptyChild;
+    n.parent = -1;
+    n.pad = 0;
+    nodes[0] = n;
+}
+
+inline unsigned int grid_for(int64_t n) { return (unsigned int)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
+    // cbounds: min = 0xffffffff, max = 0; nvalid = 0
+    hipError_t e = hipMemsetAsync(b.cbounds, 0xff, 3 * sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.cbounds + 3, 0, 3 * sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.nvalid, 0, sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    if (b.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.n, b.sqrt_mode,
+                       b.box, b.cent, b.cbounds, b.nvalid);
+    return hipGetLastError();
+}
+
+hipError_t launch_morton(const BuildBuffers &b, hipStream_t s) {
+    if (b.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_morton, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.cbounds, b.n, b.keys,
+                       b.vals);
+    return hipGetLastError();
+}
+
+size_t sort_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                              (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 64);
+    return bytes;
+}
+
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s) {
+    if (b.n == 0) return hipSuccess;
+    size_t bytes = b.sort_tmp_bytes;
+    // Morton keys use bits [0, 63); invalid beams carry ~0 and sort last either way.
+    return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n, 0, 64,
+                                     s);
+}
+
+hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
+    if (nvalid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power, b.box,
+                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.recs, b.pow);
+    return hipGetLastError();
+}
+
+hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
+    if (nvalid == 0) return hipSuccess;
+    const int K = b.leaf_size;
+    const int nleaf = (int)((nvalid + K - 1) / K);
+    if (nleaf == 1) {
+        hipLaunchKernelGGL(k_single, dim3(1), dim3(64), 0, s, b.recs, nvalid, K, b.nodes);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_karras, dim3(grid_for(nleaf - 1)), dim3(kBlock), 0, s, b.keys_alt, K, nleaf, b.nodes,
+                       b.leaf_parent);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.visit, 0, sizeof(unsigned int) * (size_t)(nleaf - 1), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_refit, dim3(grid_for(nleaf)), dim3(kBlock), 0, s, b.recs, nvalid, K, nleaf, b.nodes,
+                       b.leaf_parent, b.visit);
+    return hipGetLastError();
+}
+
+}  // namespace bre

@@ -1,0 +1,99 @@
+// bre_device.h — device data layout and kernel launchers shared by the build and gather units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bre {
+
+// One beam in BVH (sorted) order: 64 B, one cache line.  Everything the per-pair test needs
+// except the power, which is only read when a pair contributes.
+struct alignas(16) BeamRec {
+    float lo[3], hi[3];  // reference test box: WorldBound, or the union over beams with an
+                         // identical centroid (those share one SAH leaf in the reference)
+    float b0[3];         // beam start
+    float bu[3];         // (end - start) * (1/|end - start|)
+    float mag_b;         // |end - start|
+    float radius;        // beam radius (PhotonBeam::radius)
+    float pad[2];
+};
+static_assert(sizeof(BeamRec) == 64, "BeamRec must be one 64-B line");
+
+// Binary BVH interior node, 64 B: both children's boxes live in the parent so one line per
+// visit tests two children.  child >= 0: interior node index; child < 0: leaf cluster ~child;
+// kEmptyChild: no child (box is empty).
+struct alignas(16) Node {
+    float lo[2][3];
+    float hi[2][3];
+    int32_t child[2];
+    int32_t parent;
+    int32_t pad;
+};
+static_assert(sizeof(Node) == 64, "Node must be one 64-B line");
+
+constexpr int32_t kEmptyChild = INT32_MIN;
+constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
+constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
+
+// Error / counter block in device memory (zeroed per call).
+struct DevCounters {
+    unsigned long long candidates;
+    unsigned long long contributions;
+    unsigned long long node_visits;
+    unsigned int flags;  // bit0 stack overflow, bit1 pixel index out of range
+    unsigned int pad;
+};
+
+struct BuildBuffers {
+    // inputs (device)
+    const float *start, *end, *radius, *power;
+    int64_t n;
+    int sqrt_mode;
+    int leaf_size;
+    // scratch
+    float *box;        // 6n (input order)
+    float *cent;       // 3n (input order)
+    unsigned int *cbounds;  // 6 ordered-uint min/max of valid centroids
+    unsigned int *nvalid;   // 1
+    unsigned long long *keys, *keys_alt;
+    int32_t *vals, *vals_alt;
+    void *sort_tmp;
+    size_t sort_tmp_bytes;
+    int32_t *leaf_parent;  // nleaf
+    unsigned int *visit;   // nnodes counters
+    // outputs
+    BeamRec *recs;      // nvalid
+    float4 *pow;        // nvalid, powerEnd * 1e-5f
+    Node *nodes;        // max(nleaf-1, 1)
+};
+
+// build kernels (bre_build.hip)
+hipError_t launch_prep(const BuildBuffers &b, hipStream_t s);
+hipError_t launch_morton(const BuildBuffers &b, hipStream_t s);
+size_t sort_temp_bytes(int64_t n);
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s);
+hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
+hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
+
+struct GatherArgs {
+    int64_t nseg;
+    const float *o, *p, *d, *tmax;
+    const int32_t *pixel;
+    float R;
+    int64_t npix;
+    float *accum;      // may be null
+    float *seg_rgb;    // may be null
+    int32_t *seg_counts;  // may be null
+    const BeamRec *recs;
+    const float4 *pow;
+    const Node *nodes;
+    int64_t nvalid;
+    int leaf_size;
+    DevCounters *ctr;
+};
+
+// gather kernels (bre_gather.hip)
+hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStream_t s);
+hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s);
+
+}  // namespace bre

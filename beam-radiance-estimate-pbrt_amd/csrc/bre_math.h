@@ -1,0 +1,154 @@
+// bre_math.h — float arithmetic of the reference's gather path, written for gfx950 device code.
+//
+// Every function reproduces the reference's operation order and precision so that one
+// (segment, beam) pair gives bit-identical results to pbrt's x86-64 float code:
+//   * no FMA contraction: this header must be compiled with -ffp-contract=off (csrc/Makefile);
+//   * correctly rounded division and sqrt (-fhip-fp32-correctly-rounded-divide-sqrt);
+//   * Vector3 operator/ multiplies by (Float)1/f  (geometry.h:244-257);
+//   * Cross is evaluated in double and rounded to float (geometry.h:957-963);
+//   * std::min / std::max NaN behaviour is kept where it matters (Bounds3 ctor, geometry.h:759-763).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bre {
+
+struct f3 {
+    float x, y, z;
+};
+
+__host__ __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__host__ __device__ __forceinline__ f3 add3(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ __forceinline__ f3 sub3(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+// Vector3::operator*(U s) = (s*x, s*y, s*z)
+__host__ __device__ __forceinline__ f3 scale3(f3 a, float s) { return mk(s * a.x, s * a.y, s * a.z); }
+// Vector3::operator/(U f): inv = 1/f, then multiply
+__host__ __device__ __forceinline__ f3 div3(f3 a, float f) {
+    const float inv = 1.0f / f;
+    return mk(a.x * inv, a.y * inv, a.z * inv);
+}
+__host__ __device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ float lensq3(f3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__host__ __device__ __forceinline__ float len3(f3 a) { return sqrtf(lensq3(a)); }
+
+// Cross(v1, v2) in double, geometry.h:957-963
+__host__ __device__ __forceinline__ f3 cross3d(f3 v1, f3 v2) {
+    const double v1x = v1.x, v1y = v1.y, v1z = v1.z;
+    const double v2x = v2.x, v2y = v2.y, v2z = v2.z;
+    return mk((float)((v1y * v2z) - (v1z * v2y)), (float)((v1z * v2x) - (v1x * v2z)),
+              (float)((v1x * v2y) - (v1y * v2x)));
+}
+
+// Determinant, photonbeam.cpp:79-85
+__host__ __device__ __forceinline__ float det3(f3 a, f3 b, f3 c) {
+    return a.x * b.y * c.z + a.y * b.z * c.x + a.z * b.x * c.y - (a.z * b.y * c.x + a.y * b.x * c.z + a.x * b.z * c.y);
+}
+
+__host__ __device__ __forceinline__ float clampf_ref(float v, float lo, float hi) {  // pbrt.h:278-284
+    return (v < lo) ? lo : ((v > hi) ? hi : v);
+}
+__host__ __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
+__host__ __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+// 1 + 2*gamma(3) with MachineEpsilon = FLT_EPSILON/2, evaluated in float as pbrt does
+// (pbrt.h:175-176, 263-265; geometry.h:1421).
+__host__ __device__ __forceinline__ float slab_pad() {
+    const float eps = 5.96046447753906250e-08f;  // 2^-24
+    const float g3 = (3 * eps) / (1 - 3 * eps);
+    return 1 + 2 * g3;
+}
+
+// PhotonBeam::WorldBound, photonbeambvh.h:60-72.  sqrt_mode 0: `sqrt` resolves to
+// ::sqrt(double) under libstdc++, so `2*radius*sqrt(..)` and the `+` are double.
+__host__ __device__ __forceinline__ void world_bound(f3 start, f3 end, float radius, int sqrt_mode, f3 &lo, f3 &hi) {
+    f3 dir = sub3(end, start);
+    const f3 center = add3(start, div3(dir, 2.0f));
+    const float len = len3(dir);
+    dir = div3(dir, len);
+    f3 size;
+    const float tr = 2 * radius;
+    if (sqrt_mode == 0) {
+        size.x = (float)((double)(dir.x * len) + (double)tr * sqrt((double)(1 - dir.x * dir.x)));
+        size.y = (float)((double)(dir.y * len) + (double)tr * sqrt((double)(1 - dir.y * dir.y)));
+        size.z = (float)((double)(dir.z * len) + (double)tr * sqrt((double)(1 - dir.z * dir.z)));
+    } else {
+        size.x = dir.x * len + tr * sqrtf(1 - dir.x * dir.x);
+        size.y = dir.y * len + tr * sqrtf(1 - dir.y * dir.y);
+        size.z = dir.z * len + tr * sqrtf(1 - dir.z * dir.z);
+    }
+    const f3 half = div3(size, 2.0f);
+    const f3 p1 = sub3(center, half), p2 = add3(center, half);
+    lo = mk(smin(p1.x, p2.x), smin(p1.y, p2.y), smin(p1.z, p2.z));
+    hi = mk(smax(p1.x, p2.x), smax(p1.y, p2.y), smax(p1.z, p2.z));
+}
+
+// Bounds3::IntersectP(ray, invDir, dirIsNeg), geometry.h:1410-1436.  `inv` selects which inverse
+// direction is used: the exact one reproduces the reference test; the sanitised one gives a test
+// that is monotone under box containment (used for BVH interior nodes, which are unions).
+// Box coordinates are passed by value so that wave-uniform boxes stay in SGPRs and the per-lane
+// dirIsNeg choice is a register select, not a per-lane address.
+struct Box6 {
+    float lx, ly, lz, hx, hy, hz;
+};
+__host__ __device__ __forceinline__ bool slab_test(const Box6 &b, f3 o, f3 inv, int n0, int n1, int n2, float ray_tmax,
+                                                   float *t_entry) {
+    const float pad = slab_pad();
+    float tMin = ((n0 ? b.hx : b.lx) - o.x) * inv.x;
+    float tMax = ((n0 ? b.lx : b.hx) - o.x) * inv.x;
+    const float tyMin = ((n1 ? b.hy : b.ly) - o.y) * inv.y;
+    float tyMax = ((n1 ? b.ly : b.hy) - o.y) * inv.y;
+    tMax *= pad;
+    tyMax *= pad;
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    const float tzMin = ((n2 ? b.hz : b.lz) - o.z) * inv.z;
+    float tzMax = ((n2 ? b.lz : b.hz) - o.z) * inv.z;
+    tzMax *= pad;
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    if (t_entry) *t_entry = tMin;
+    return (tMin < ray_tmax) && (tMax > 0);
+}
+
+// ComputeClosestPoints, photonbeam.cpp:87-186, specialised to precomputed unit directions:
+//   segment A: a0, a1, au = (a1-a0)*(1/|A|), mag_a = |a1-a0|
+//   beam    B: b0, bu = (b1-b0)*(1/|B|), mag_b = |b1-b0| (> 0: zero-length beams have a NaN
+//              WorldBound and never become candidates, so the magB==0 branch is unreachable)
+// Returns false for parallel lines (no contribution).  Writes |aClosest - bClosest|.
+__host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu, float mag_b,
+                                                          float &dist) {
+    if (mag_a == 0.0f) {
+        // A is a point: project a0 onto B, clamp (photonbeam.cpp:95-108)
+        const float d = dot3(sub3(a0, b0), bu);
+        const f3 bc = add3(b0, scale3(bu, clampf_ref(d, 0.0f, mag_b)));
+        dist = len3(sub3(a0, bc));
+        return true;
+    }
+    const f3 cr = cross3d(au, bu);
+    const float denom = lensq3(cr);
+    if (denom == 0.0f) return false;  // parallel (photonbeam.cpp:131-156)
+    const f3 t = sub3(b0, a0);
+    const float detA = det3(t, bu, cr);
+    const float detB = det3(t, au, cr);
+    const float t0 = detA / denom;
+    const float t1 = detB / denom;
+    f3 pA = add3(a0, scale3(au, t0));
+    f3 pB = add3(b0, scale3(bu, t1));
+    if (t0 < 0) pA = a0;
+    else if (t0 > mag_a) pA = a1;
+    if (t0 < 0 || t0 > mag_a) {
+        const float d = clampf_ref(dot3(bu, sub3(pA, b0)), 0.0f, mag_b);
+        pB = add3(b0, scale3(bu, d));
+    }
+    if (t1 < 0 || t1 > mag_b) {
+        const float d = clampf_ref(dot3(au, sub3(pB, a0)), 0.0f, mag_a);
+        pA = add3(a0, scale3(au, d));
+    }
+    dist = len3(sub3(pA, pB));
+    return true;
+}
+
+}  // namespace bre

@@ -1,0 +1,93 @@
+// photonbeam_gpu.cpp — see photonbeam_gpu.h.
+#include "photonbeam_gpu.h"
+
+namespace bre_host {
+
+void SegmentRecorder::Clear() {
+    o_.clear();
+    p_.clear();
+    d_.clear();
+    tmax_.clear();
+    pixel_.clear();
+}
+
+void SegmentRecorder::Record(const CameraSegment &s) {
+    o_.insert(o_.end(), {s.o.x, s.o.y, s.o.z});
+    p_.insert(p_.end(), {s.p.x, s.p.y, s.p.z});
+    d_.insert(d_.end(), {s.d.x, s.d.y, s.d.z});
+    tmax_.push_back(s.tMax);
+    pixel_.push_back(s.pixel);
+}
+
+PhotonBeamGpuBVH::PhotonBeamGpuBVH(int device) {
+    bre_status st = bre_create(device, &ctx_);
+    if (st != BRE_OK) {
+        ctx_ = nullptr;
+        err_ = "bre_create failed with status " + std::to_string((int)st);
+    }
+}
+
+PhotonBeamGpuBVH::~PhotonBeamGpuBVH() { bre_destroy(ctx_); }
+
+bool PhotonBeamGpuBVH::Check(bre_status st) {
+    if (st == BRE_OK) return true;
+    err_ = ctx_ ? bre_last_error(ctx_) : "no context";
+    return false;
+}
+
+bool PhotonBeamGpuBVH::SetOption(bre_option opt, int64_t value) {
+    if (!ctx_) return false;
+    return Check(bre_set_option(ctx_, opt, value));
+}
+
+bool PhotonBeamGpuBVH::Stats(bre_stats *out) const { return ctx_ && bre_get_stats(ctx_, out) == BRE_OK; }
+
+bool PhotonBeamGpuBVH::Build(const std::vector<PhotonBeam> &beams) {
+    if (!ctx_) return false;
+    const size_t n = beams.size();
+    std::vector<float> s(3 * n), e(3 * n), r(n), pw(3 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const PhotonBeam &b = beams[i];
+        s[3 * i] = b.start.x; s[3 * i + 1] = b.start.y; s[3 * i + 2] = b.start.z;
+        e[3 * i] = b.end.x; e[3 * i + 1] = b.end.y; e[3 * i + 2] = b.end.z;
+        r[i] = b.radius;
+        pw[3 * i] = b.powerEnd.x; pw[3 * i + 1] = b.powerEnd.y; pw[3 * i + 2] = b.powerEnd.z;
+    }
+    return Check(bre_set_beams(ctx_, (int64_t)n, s.data(), e.data(), r.data(), pw.data()));
+}
+
+bool PhotonBeamGpuBVH::Gather(const SegmentRecorder &segs, float currentBeamRadius, std::vector<float> &pixelLd) {
+    if (!ctx_) return false;
+    const int64_t npix = (int64_t)(pixelLd.size() / 3);
+    return Check(bre_gather(ctx_, segs.Size(), segs.O(), segs.P(), segs.D(), segs.TMax(), segs.Pixel(),
+                            currentBeamRadius, npix, pixelLd.data(), nullptr, nullptr));
+}
+
+PhotonBeamParams PhotonBeamParams::FromLookup(const Lookup &ps, bool quickRender, int pixelCount) {
+    PhotonBeamParams p;
+    p.nIterations = ps.findInt("iterations", ps.findInt("numiterations", 64));
+    p.startIteration = ps.findInt("startiteration", 0);
+    p.endIteration = ps.findInt("enditeration", p.nIterations);
+    p.maxDepth = ps.findInt("maxdepth", 5);
+    p.photonsPerIteration = ps.findInt("photonsperiteration", -1);
+    p.writeFrequency = ps.findInt("imagewritefrequency", 1 << 31);
+    p.initialBeamRadius = ps.findFloat("initialbeamradius", 1.f);
+    p.alpha = ps.findFloat("alpha", 0.5f);
+    // like the reference, --quick shrinks nIterations after endIteration was already defaulted
+    if (quickRender) p.nIterations = p.nIterations / 16 > 1 ? p.nIterations / 16 : 1;
+    p.renderSurfaces = ps.findBool("rendersurfaces", true);
+    p.renderMedia = ps.findBool("rendermedia", true);
+    if (p.photonsPerIteration <= 0) p.photonsPerIteration = pixelCount;
+    return p;
+}
+
+float BeamRadiusAt(const PhotonBeamParams &p, int iteration) {
+    return bre_beam_radius_at(p.initialBeamRadius, p.alpha, iteration);
+}
+
+void ResolveImage(const std::vector<float> &pixelLd, int iteration, std::vector<float> &rgb) {
+    rgb.resize(pixelLd.size());
+    bre_resolve_image((int64_t)(pixelLd.size() / 3), pixelLd.data(), iteration, rgb.data());
+}
+
+}  // namespace bre_host

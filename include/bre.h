@@ -1,0 +1,134 @@
+/*
+ * bre.h — C ABI of the MI355X beam-radiance-estimate (photon-beam gather) library, libbre.so.
+ *
+ * Drop-in boundary for the hot path of bwiberg/beam-radiance-estimate-pbrt:
+ *
+ *   reference (pbrt-v3 fork)                                   this ABI
+ *   ---------------------------------------------------------  ---------------------------------
+ *   PhotonBeamBVH photonBeamBVH(std::move(photonBeams));       bre_set_beams / bre_set_beams_device
+ *     src/integrators/photonbeam.cpp:438,                        (copy + GPU build; the beam set and
+ *     ctor src/core/photonbeambvh.cpp:204-248                    BVH live on the device until replaced)
+ *   photonBeamBVH.Intersect(ray) + ComputeClosestPoints +      bre_gather / bre_gather_device
+ *     `pixel.Ld += 1e-5 * powerEnd * sqrt(1 - r*r)`             (all camera segments of one iteration
+ *     src/integrators/photonbeam.cpp:494-508,                    in one call; += into per-pixel RGB)
+ *     src/core/photonbeambvh.cpp:685-723
+ *   currentBeamRadius (photonbeam.cpp:354-356, 562)            argument `beam_radius_cur` (R_cur)
+ *   PhotonBeam{start,end,radius,powerStart,powerEnd}           SoA/xyz float arrays below
+ *     src/core/photonbeambvh.h:48-73                             (powerStart is always 0 in the
+ *                                                                reference, photonbeam.cpp:266,292,
+ *                                                                and unused by the gather)
+ *
+ * A "segment" is one camera-ray segment of the reference's camera pass: ray.o, ray.d and
+ * ray.tMax after Scene::Intersect (primitive.cpp:101 sets tMax to the hit) and isect.p.
+ * All four are needed: the candidate test uses (o, d, tMax) (Bounds3::IntersectP,
+ * geometry.h:1410-1436) and the closest-point kernel uses the segment [o, isect.p]
+ * (photonbeam.cpp:499).
+ *
+ * Semantics are the reference's, bit for bit per (segment, beam) pair (see DESIGN.md "parity
+ * contract"): candidate set = beams whose WorldBound box (group box for beams with identical
+ * centroids) passes the gamma(3)-padded slab test; contribution 1e-5*powerEnd*sqrt(1-(d/(R+r))^2)
+ * for d < R + r, no phase, no camera throughput.  Only the float summation order differs.
+ *
+ * Conventions: plain pointers and sizes; xyz arrays are interleaved float[3*n]; RGB arrays
+ * float[3*n].  No exceptions cross the ABI; every call returns a bre_status and stores a message
+ * retrievable with bre_last_error().  One context per GPU; a context is not thread-safe.
+ * Errors follow pbrt's style of "report and continue" only in the sense that a failed call leaves
+ * the context usable; no function aborts the process.
+ */
+#ifndef BRE_H
+#define BRE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BRE_ABI_VERSION 1
+
+typedef struct bre_ctx bre_ctx;
+
+typedef enum bre_status {
+    BRE_OK = 0,
+    BRE_ERR_INVALID_ARG = 1, /* null pointer, negative size, pixel index out of range ... */
+    BRE_ERR_HIP = 2,         /* a HIP runtime call failed (message has the HIP error string) */
+    BRE_ERR_OOM = 3,         /* device allocation failed */
+    BRE_ERR_STATE = 4,       /* e.g. bre_gather before any bre_set_beams */
+    BRE_ERR_NO_DEVICE = 5    /* no HIP device / bad device ordinal */
+} bre_status;
+
+/* Options for bre_set_option(). */
+typedef enum bre_option {
+    BRE_OPT_COUNTERS = 1,    /* 0/1: per-segment candidate / contribution / node-visit counting */
+    BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
+    BRE_OPT_KERNEL = 3,      /* 0 = auto, 1 = wave-packet traversal, 2 = thread-per-segment */
+    BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 4); applies at next build */
+    BRE_OPT_SQRT_MODE = 5    /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
+} bre_option;
+
+typedef struct bre_stats {
+    int64_t n_beams;         /* beams in the current set (after set_beams) */
+    int64_t n_beams_valid;   /* beams with a finite WorldBound (zero-length beams have a NaN box) */
+    int64_t n_nodes;         /* BVH interior nodes */
+    int64_t n_segments;      /* segments in the last gather */
+    int64_t candidates;      /* sum over segments of C = beams passing the reference box test
+                                (= size of PhotonBeamBVH::Intersect's result); counters only */
+    int64_t contributions;   /* pairs with d < R + r that added to the pixel; counters only */
+    int64_t node_visits;     /* interior-node visits summed over waves (kernel 1) or threads
+                                (kernel 2); counters only */
+    double build_ms;         /* device time of the last BVH build (timing only) */
+    double gather_ms;        /* device time of the last gather kernel (timing only) */
+} bre_stats;
+
+/* ---- context ---- */
+bre_status bre_create(int device, bre_ctx **out);
+void bre_destroy(bre_ctx *ctx);
+const char *bre_last_error(const bre_ctx *ctx);
+int bre_abi_version(void);
+bre_status bre_set_option(bre_ctx *ctx, int option, int64_t value);
+/* Use an existing hipStream_t (cast to void*) for all work of this context; NULL = the
+   context's own stream.  The caller keeps ownership of a stream it passes in. */
+bre_status bre_set_stream(bre_ctx *ctx, void *hip_stream);
+bre_status bre_synchronize(bre_ctx *ctx);
+bre_status bre_get_stats(const bre_ctx *ctx, bre_stats *out);
+
+/* ---- beams (replaces `PhotonBeamBVH photonBeamBVH(std::move(photonBeams))`) ----
+   start_xyz, end_xyz: float[3n]; radius: float[n]; power_end_rgb: float[3n].
+   bre_set_beams copies host arrays; bre_set_beams_device reads device arrays (no copy kept:
+   the build consumes them before returning control of the stream).  n = 0 clears the set
+   (every gather then adds nothing, as an empty PhotonBeamBVH returns no beams). */
+bre_status bre_set_beams(bre_ctx *ctx, int64_t n, const float *start_xyz, const float *end_xyz,
+                         const float *radius, const float *power_end_rgb);
+bre_status bre_set_beams_device(bre_ctx *ctx, int64_t n, const float *d_start_xyz,
+                                const float *d_end_xyz, const float *d_radius,
+                                const float *d_power_end_rgb);
+
+/* ---- gather (replaces photonbeam.cpp:494-508 for every segment of an iteration) ----
+   seg_o_xyz, seg_p_xyz, seg_d_xyz: float[3*nseg] (ray.o, isect.p, ray.d); seg_tmax: float[nseg]
+   (ray.tMax); seg_pixel: int32[nseg], pixel index in [0, npix).
+   accum_rgb: float[3*npix], accumulated (+=) like PhotonBeamPixel::Ld (may be NULL).
+   seg_rgb: float[3*nseg] per-segment sums, overwritten (may be NULL).
+   seg_counts: int32[2*nseg] per-segment {C candidates, contributions} (may be NULL; needs
+   BRE_OPT_COUNTERS=1).  beam_radius_cur: the integrator's currentBeamRadius R_cur.
+   bre_gather takes host pointers (PCIe copies in and out, synchronous); bre_gather_device
+   takes device pointers and is asynchronous on the context's stream. */
+bre_status bre_gather(bre_ctx *ctx, int64_t nseg, const float *seg_o_xyz, const float *seg_p_xyz,
+                      const float *seg_d_xyz, const float *seg_tmax, const int32_t *seg_pixel,
+                      float beam_radius_cur, int64_t npix, float *accum_rgb, float *seg_rgb,
+                      int32_t *seg_counts);
+bre_status bre_gather_device(bre_ctx *ctx, int64_t nseg, const float *d_seg_o_xyz,
+                             const float *d_seg_p_xyz, const float *d_seg_d_xyz,
+                             const float *d_seg_tmax, const int32_t *d_seg_pixel,
+                             float beam_radius_cur, int64_t npix, float *d_accum_rgb,
+                             float *d_seg_rgb, int32_t *d_seg_counts);
+
+/* ---- integrator helpers (photonbeam.cpp:354-356, 562, 578) ---- */
+/* R_i for iteration i: R_{k+1} = R_k * (k + alpha) / (k + 1), R_0 = initial, in float. */
+float bre_beam_radius_at(float initial_radius, float alpha, int iteration);
+/* image = Ld / (iter + 1) for npix pixels (host arrays). */
+bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, float *out_rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BRE_H */

@@ -1,0 +1,140 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle_bre.so) — test infrastructure only.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle_bre.so")
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class Oracle:
+    def __init__(self, lib):
+        self.lib = lib
+        P, I64, I32, F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+        lib.ora_slab_pad.restype = F
+        lib.ora_beam_bounds.argtypes = [I64, P, P, P, I32, P]
+        lib.ora_closest_points.argtypes = [P, P, P, P, P, P]
+        lib.ora_closest_points.restype = I32
+        lib.ora_intersect_box.argtypes = [P, P, P, F]
+        lib.ora_intersect_box.restype = I32
+        lib.ora_radius_at.argtypes = [F, F, I32]
+        lib.ora_radius_at.restype = F
+        lib.ora_bvh_build.argtypes = [I64, P, P, P, P, I32]
+        lib.ora_bvh_build.restype = P
+        lib.ora_bvh_node_count.argtypes = [P]
+        lib.ora_bvh_node_count.restype = I64
+        lib.ora_bvh_max_leaf.argtypes = [P]
+        lib.ora_bvh_max_leaf.restype = I32
+        lib.ora_bvh_free.argtypes = [P]
+        lib.ora_gather.argtypes = [P, I64, P, P, P, P, P, F, P, P, P, P, P, I32, I64]
+        lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P]
+
+    # -- primitives --
+    def slab_pad(self) -> float:
+        return float(self.lib.ora_slab_pad())
+
+    def beam_bounds(self, start, end, radius, sqrt_mode=0):
+        start, end, radius = (np.ascontiguousarray(x, np.float32) for x in (start, end, radius))
+        n = radius.shape[0]
+        box = np.zeros((n, 6), np.float32)
+        self.lib.ora_beam_bounds(n, _p(start), _p(end), _p(radius), sqrt_mode, _p(box))
+        return box
+
+    def closest_points(self, a0, a1, b0, b1):
+        a0, a1, b0, b1 = (np.ascontiguousarray(x, np.float32) for x in (a0, a1, b0, b1))
+        ac = np.zeros(3, np.float32)
+        bc = np.zeros(3, np.float32)
+        ok = self.lib.ora_closest_points(_p(a0), _p(a1), _p(b0), _p(b1), _p(ac), _p(bc))
+        return bool(ok), ac, bc
+
+    def intersect_box(self, box, o, d, tmax):
+        box, o, d = (np.ascontiguousarray(x, np.float32) for x in (box, o, d))
+        return bool(self.lib.ora_intersect_box(_p(box), _p(o), _p(d), float(tmax)))
+
+    def radius_at(self, r0, alpha, it):
+        return float(self.lib.ora_radius_at(r0, alpha, it))
+
+    # -- gather through the reference SAH tree --
+    def build(self, beams, sqrt_mode=0):
+        return OracleBVH(self, beams, sqrt_mode)
+
+    def bruteforce(self, beams, segs, R, sqrt_mode=0):
+        b = {k: np.ascontiguousarray(beams[k], np.float32) for k in ("start", "end", "radius", "power")}
+        s = {k: np.ascontiguousarray(segs[k], np.float32) for k in ("o", "p", "d", "tmax")}
+        nb, ns = b["radius"].shape[0], s["tmax"].shape[0]
+        rgb = np.zeros((ns, 3), np.float32)
+        cand = np.zeros(ns, np.int64)
+        contrib = np.zeros(ns, np.int64)
+        self.lib.ora_gather_bruteforce(nb, _p(b["start"]), _p(b["end"]), _p(b["radius"]), _p(b["power"]), sqrt_mode,
+                                       ns, _p(s["o"]), _p(s["p"]), _p(s["d"]), _p(s["tmax"]), float(R), _p(rgb),
+                                       _p(cand), _p(contrib))
+        return {"seg_rgb": rgb, "cand": cand, "contrib": contrib}
+
+
+class OracleBVH:
+    def __init__(self, ora: Oracle, beams, sqrt_mode=0):
+        self.ora = ora
+        self.b = {k: np.ascontiguousarray(beams[k], np.float32) for k in ("start", "end", "radius", "power")}
+        n = self.b["radius"].shape[0]
+        self.h = ora.lib.ora_bvh_build(n, _p(self.b["start"]), _p(self.b["end"]), _p(self.b["radius"]),
+                                       _p(self.b["power"]), sqrt_mode)
+
+    def node_count(self):
+        return int(self.ora.lib.ora_bvh_node_count(self.h))
+
+    def max_leaf(self):
+        return int(self.ora.lib.ora_bvh_max_leaf(self.h))
+
+    def gather(self, segs, R, npix=None, nthreads=1, chunk=256):
+        s = {k: np.ascontiguousarray(segs[k], np.float32) for k in ("o", "p", "d", "tmax")}
+        ns = s["tmax"].shape[0]
+        pix = np.ascontiguousarray(segs["pixel"], np.int32) if "pixel" in segs else None
+        rgb = np.zeros((ns, 3), np.float32)
+        cand = np.zeros(ns, np.int64)
+        vis = np.zeros(ns, np.int64)
+        contrib = np.zeros(ns, np.int64)
+        accum = None
+        if npix is not None:
+            accum = np.zeros((npix, 3), np.float32)
+        self.ora.lib.ora_gather(self.h, ns, _p(s["o"]), _p(s["p"]), _p(s["d"]), _p(s["tmax"]), _p(pix), float(R),
+                                _p(rgb), _p(accum), _p(cand), _p(vis), _p(contrib), int(nthreads), int(chunk))
+        out = {"seg_rgb": rgb, "cand": cand, "visit": vis, "contrib": contrib}
+        if accum is not None:
+            out["accum"] = accum
+        return out
+
+    def close(self):
+        if self.h:
+            self.ora.lib.ora_bvh_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_ORACLE = None
+
+
+def load_oracle() -> Oracle:
+    global _ORACLE
+    if _ORACLE is None:
+        src = os.path.join(ORACLE_DIR, "bre_oracle.cpp")
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+            subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+        _ORACLE = Oracle(ctypes.CDLL(ORACLE_SO))
+    return _ORACLE

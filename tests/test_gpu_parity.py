@@ -1,0 +1,222 @@
+"""GPU parity: libbre (HIP, gfx950) against the CPU oracle on the same seeded inputs.
+
+Bar (DESIGN.md "parity contract"):
+* candidate count C and contribution count per segment: EXACT (integer work: the candidate set is
+  the reference's, pair by pair);
+* per-segment RGB: relative error <= 1e-5 of the segment's magnitude (float summation order
+  differs from the reference's DFS order; every individual pair is bit-identical);
+* image: relative L2 <= 1e-3 (north star), in practice ~1e-7.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEG_RTOL = 1e-5
+
+
+def _seg_close(gpu, ref, rtol=SEG_RTOL):
+    scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-30)
+    err = (np.abs(gpu - ref) / scale).max()
+    return err
+
+
+def _rel_l2(a, b):
+    den = np.sqrt((b.astype(np.float64) ** 2).sum())
+    return float(np.sqrt(((a.astype(np.float64) - b) ** 2).sum()) / max(den, 1e-300))
+
+
+@pytest.fixture(scope="module")
+def ctxs(bre):
+    out = {}
+    for k in (1, 2):
+        out[k] = bre.BeamGather(0, counters=True, kernel=k)
+    yield out
+    for c in out.values():
+        c.close()
+
+
+@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("leaf", [1, 4, 8])
+def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
+    beams = synth.fog_beams(3000, seed=12345)
+    segs = synth.camera_segments(48, 40, seed=777)
+    R = 0.01
+    ref = oracle.build(beams).gather(segs, R)
+    with bre.BeamGather(0, counters=True, kernel=kernel, leaf_size=leaf) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, counts=True)
+        st = g.stats()
+    assert np.array_equal(out["counts"][:, 0], ref["cand"]), "candidate sets differ"
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"]), "contribution sets differ"
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    assert st["candidates"] == int(ref["cand"].sum())
+    assert st["contributions"] == int(ref["contrib"].sum())
+
+
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_bounce_segments_match_oracle(bre, synth, oracle, kernel):
+    beams = synth.fog_beams(3000, seed=99)
+    segs = synth.bounce_segments(3000, seed=5)
+    R = 0.013
+    ref = oracle.build(beams).gather(segs, R)
+    with bre.BeamGather(0, counters=True, kernel=kernel) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, counts=True)
+    assert np.array_equal(out["counts"][:, 0], ref["cand"])
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+def test_pixel_accumulation_and_image_l2(bre, synth, oracle):
+    """Several segments per pixel (camera path depths) accumulate like PhotonBeamPixel::Ld."""
+    beams = synth.fog_beams(2000, seed=3)
+    cam = synth.camera_segments(32, 32, seed=4)
+    bnc = synth.bounce_segments(2048, seed=6, npix=1024)
+    segs = {k: np.concatenate([cam[k], bnc[k]]) for k in cam}
+    R = 0.01
+    ref = oracle.build(beams).gather(segs, R, npix=1024)
+    accum = np.zeros((1024, 3), np.float32)
+    with bre.BeamGather(0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, npix=1024, accum=accum,
+                 seg_rgb=False)
+    assert _rel_l2(accum, ref["accum"]) <= 1e-6
+
+
+def test_empty_beam_set(bre, synth):
+    segs = synth.camera_segments(8, 8)
+    accum = np.ones((64, 3), np.float32)
+    with bre.BeamGather(0, counters=True) as g:
+        g.set_beams(np.zeros((0, 3)), np.zeros((0, 3)), np.zeros(0), np.zeros((0, 3)))
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=0.01, npix=64, accum=accum,
+                       counts=True)
+    assert not out["seg_rgb"].any() and not out["counts"].any()
+    assert (accum == 1).all()
+
+
+def test_single_beam_and_tiny_sets(bre, synth, oracle):
+    for n in (1, 2, 3, 5, 17):
+        beams = synth.fog_beams(n, seed=100 + n, mean_length=0.6)
+        segs = synth.bounce_segments(2000, seed=n)
+        ref = oracle.build(beams).gather(segs, 0.05)
+        with bre.BeamGather(0, counters=True) as g:
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.05, counts=True)
+        assert np.array_equal(out["counts"][:, 0], ref["cand"]), n
+        assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+def test_duplicate_centroids_use_group_box(bre, synth, oracle):
+    """Beams with bit-identical centroids share one SAH leaf in the reference, whose union box is
+    tested (photonbeambvh.cpp:289-297); libbre reproduces that with group boxes."""
+    base = synth.fog_beams(400, seed=8, mean_length=0.3)
+    start, end = base["start"].copy(), base["end"].copy()
+    # mirror every 4th beam around its centre: same centroid, different (quirky) box
+    idx = np.arange(0, 400, 4)
+    rev_s, rev_e = end[idx].copy(), start[idx].copy()
+    beams = {
+        "start": np.concatenate([start, rev_s]), "end": np.concatenate([end, rev_e]),
+        "radius": np.full(500, 0.02, np.float32),
+        "power": np.concatenate([base["power"], base["power"][idx]]),
+    }
+    segs = synth.bounce_segments(3000, seed=9)
+    bvh = oracle.build(beams)
+    ref = bvh.gather(segs, 0.02)
+    bf = oracle.bruteforce(beams, segs, 0.02)
+    assert np.array_equal(ref["cand"], bf["cand"])
+    with bre.BeamGather(0, counters=True) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
+    assert np.array_equal(out["counts"][:, 0], ref["cand"])
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+
+
+def test_axis_aligned_rays_and_degenerate_segments(bre, oracle):
+    """Zero direction components (inf/NaN slab values) and zero-length segments."""
+    rng = np.random.default_rng(1)
+    n = 500
+    start = rng.random((n, 3), dtype=np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[::3, 0] = 0  # some axis-aligned beams
+    end = (start + 0.2 * d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    beams = {"start": start, "end": end, "radius": np.full(n, 0.03, np.float32),
+             "power": rng.random((n, 3), dtype=np.float32)}
+    m = 3000
+    o = np.round(rng.random((m, 3)) * 16).astype(np.float32) / 16  # origins on box planes often
+    dd = rng.normal(size=(m, 3)).astype(np.float32)
+    dd[0::2, 1] = 0.0
+    dd[0::3, 2] = 0.0
+    dd[5::7, 0] = -0.0
+    dd /= np.maximum(np.linalg.norm(dd, axis=1, keepdims=True), 1e-6)
+    t = rng.random(m).astype(np.float32)
+    t[::11] = 0.0  # zero-length segments: p == o
+    p = (o + dd * t[:, None]).astype(np.float32)
+    segs = {"o": o, "p": p, "d": dd.astype(np.float32), "tmax": t}
+    ref = oracle.build(beams).gather(segs, 0.02)
+    with bre.BeamGather(0, counters=True) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        for k in (1, 2):
+            g.set_option(bre.OPT_KERNEL, k)
+            out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
+            assert np.array_equal(out["counts"][:, 0], ref["cand"]), k
+            assert np.array_equal(out["counts"][:, 1], ref["contrib"]), k
+            assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+def test_zero_length_beams_never_gathered(bre, synth, oracle):
+    beams = synth.fog_beams(300, seed=21)
+    beams["end"][::10] = beams["start"][::10]  # WorldBound is NaN (0 * inf)
+    segs = synth.bounce_segments(2000, seed=22)
+    bf = oracle.bruteforce(beams, segs, 0.02)
+    with bre.BeamGather(0, counters=True) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
+        assert g.stats()["n_beams_valid"] == 270
+    assert np.array_equal(out["counts"][:, 0], bf["cand"])
+    assert _seg_close(out["seg_rgb"], bf["seg_rgb"]) <= SEG_RTOL
+
+
+def test_pixel_out_of_range_is_an_error(bre, synth):
+    beams = synth.fog_beams(100)
+    segs = synth.camera_segments(4, 4)
+    with bre.BeamGather(0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        with pytest.raises(bre.BreError):
+            g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=0.01, npix=8,
+                     accum=np.zeros((8, 3), np.float32))
+
+
+def test_device_api_matches_host_api(bre, synth):
+    import torch
+
+    beams = synth.fog_beams(5000, seed=31)
+    segs = synth.camera_segments(64, 64, seed=32)
+    dev = {k: torch.from_numpy(v).cuda().contiguous() for k, v in beams.items()}
+    dseg = {k: torch.from_numpy(v).cuda().contiguous() for k, v in segs.items()}
+    with bre.BeamGather(0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        host = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)["seg_rgb"]
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    with bre.BeamGather(0) as g:
+        g.set_stream(stream.cuda_stream)
+        g.set_beams_device(dev["start"], dev["end"], dev["radius"], dev["power"])
+        out = torch.zeros((4096, 3), dtype=torch.float32, device="cuda")
+        acc = torch.zeros((4096, 3), dtype=torch.float32, device="cuda")
+        g.gather_device(dseg["o"], dseg["p"], dseg["d"], dseg["tmax"], dseg["pixel"], 0.01, 4096, accum=acc,
+                        seg_rgb=out)
+        torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), host)
+    assert np.array_equal(acc.cpu().numpy(), host)  # one segment per pixel: single add each
+
+
+def test_deterministic_per_segment(bre, synth):
+    beams = synth.fog_beams(20000, seed=41)
+    segs = synth.camera_segments(64, 64, seed=42)
+    with bre.BeamGather(0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        a = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)["seg_rgb"]
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        b = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)["seg_rgb"]
+    assert np.array_equal(a, b)
