@@ -137,14 +137,7 @@ def bounce_segments(n: int, seed: int = 778, npix: int | None = None):
 
 
 def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16) -> np.ndarray:
-    """Pixels of the 16x16 image tiles owned by `rank` when tiles are dealt round-robin
-    (the reference's camera pass tiles, photonbeam.cpp:345-347), in tile order."""
-    ntx = (w + tile - 1) // tile
-    nty = (h + tile - 1) // tile
-    out = []
-    for t in range(rank, ntx * nty, world):
-        tx, ty = t % ntx, t // ntx
-        xs = np.arange(tx * tile, min(tx * tile + tile, w))
-        ys = np.arange(ty * tile, min(ty * tile + tile, h))
-        out.append((ys[:, None] * w + xs[None, :]).ravel())
-    return np.concatenate(out) if out else np.zeros(0, dtype=np.int64)
+    """Pixels of the 16x16 tiles owned by `rank` (see dist.tile_pixels)."""
+    from .dist import tile_pixels as _tp
+
+    return _tp(w, h, rank, world, tile)

@@ -61,6 +61,7 @@ def main():
 
     bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
     synth = importlib.import_module("beam-radiance-estimate-pbrt_amd.synth")
+    dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,14 +74,15 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     W, H = args.width, args.height * world
-    npix = W * H
-    pixels = synth.tile_pixels(W, H, rank, world)
+    frame = dmod.ShardedFrame(W, H, rank, world, device=dev)
+    npix = frame.npix
+    pixels = frame.pixels
     beams = synth.fog_beams(args.beams, seed=12345, radius=args.radius)
     segs = synth.camera_segments(W, H, seed=777, pixels=pixels)
     nseg = int(segs["tmax"].shape[0])
     dB = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in beams.items()}
     dS = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in segs.items()}
-    accum = torch.zeros((npix, 3), dtype=torch.float32, device=dev)
+    accum = frame.accum
 
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
@@ -97,8 +99,7 @@ def main():
         g.gather_device(dS["o"], dS["p"], dS["d"], dS["tmax"], dS["pixel"], R, npix, accum=accum)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
-            dist.reduce(accum, dst=0)
+        frame.reduce_to_root(0)  # one RCCL reduce per written image (no-op at N=1)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,57 @@
+"""Golden fixture (tests/golden/gather_golden.npz, made by tests/golden/make_golden.py from the
+oracle on seeded synthetic-fog inputs): the oracle must keep reproducing it bit for bit (CPU), and
+libbre must match it (GPU: exact candidate/contribution counts, per-segment RGB within 1e-5)."""
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gather_golden.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    z = np.load(GOLD)  # allow_pickle=False (default)
+    return {k: z[k] for k in z.files}
+
+
+def beams_of(g):
+    return {"start": g["beam_start"], "end": g["beam_end"], "radius": g["beam_radius"], "power": g["beam_power"]}
+
+
+def segs_of(g):
+    return {"o": g["seg_o"], "p": g["seg_p"], "d": g["seg_d"], "tmax": g["seg_tmax"], "pixel": g["seg_pixel"]}
+
+
+def test_generator_still_produces_fixture_inputs(gold, synth):
+    b = synth.fog_beams(1000, seed=12345, radius=0.02, mean_length=0.3)
+    assert np.array_equal(b["start"], gold["beam_start"]) and np.array_equal(b["end"], gold["beam_end"])
+    cam = synth.camera_segments(32, 32, seed=777)
+    assert np.array_equal(cam["p"], gold["seg_p"][:1024])
+
+
+def test_oracle_reproduces_golden(gold, oracle):
+    out = oracle.build(beams_of(gold)).gather(segs_of(gold), float(gold["R"][0]), npix=1024)
+    assert np.array_equal(out["cand"], gold["cand"])
+    assert np.array_equal(out["contrib"], gold["contrib"])
+    assert np.array_equal(out["visit"], gold["visit"])
+    assert np.array_equal(out["seg_rgb"], gold["seg_rgb"])
+    assert np.array_equal(out["accum"], gold["accum"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_gpu_matches_golden(gold, bre, kernel):
+    s = segs_of(gold)
+    accum = np.zeros((1024, 3), np.float32)
+    with bre.BeamGather(0, counters=True, kernel=kernel) as g:
+        b = beams_of(gold)
+        g.set_beams(b["start"], b["end"], b["radius"], b["power"])
+        out = g.gather(s["o"], s["p"], s["d"], s["tmax"], s["pixel"], R=float(gold["R"][0]), npix=1024,
+                       accum=accum, counts=True)
+    assert np.array_equal(out["counts"][:, 0], gold["cand"])
+    assert np.array_equal(out["counts"][:, 1], gold["contrib"])
+    scale = np.maximum(np.abs(gold["seg_rgb"]).max(axis=1, keepdims=True), 1e-30)
+    assert (np.abs(out["seg_rgb"] - gold["seg_rgb"]) / scale).max() <= 1e-5
+    rel_l2 = np.linalg.norm(accum - gold["accum"]) / np.linalg.norm(gold["accum"])
+    assert rel_l2 <= 1e-3  # north-star image tolerance (observed ~1e-7)
