@@ -22,7 +22,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "bre.h")
 BRE_OK = 0
 STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE_ERR_OOM",
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
-OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE = 1, 2, 3, 4, 5
+OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -43,7 +43,10 @@ class Stats(ctypes.Structure):
     _fields_ = [("n_beams", ctypes.c_int64), ("n_beams_valid", ctypes.c_int64),
                 ("n_nodes", ctypes.c_int64), ("n_segments", ctypes.c_int64),
                 ("candidates", ctypes.c_int64), ("contributions", ctypes.c_int64),
-                ("node_visits", ctypes.c_int64), ("build_ms", ctypes.c_double),
+                ("node_visits", ctypes.c_int64), ("leaf_visits", ctypes.c_int64),
+                ("beam_evals", ctypes.c_int64), ("ccp_wave_evals", ctypes.c_int64),
+                ("prefilter_rejects", ctypes.c_int64), ("useful_beam_evals", ctypes.c_int64),
+                ("build_ms", ctypes.c_double),
                 ("gather_ms", ctypes.c_double)]
 
     def as_dict(self):
@@ -118,7 +121,8 @@ class BeamGather:
     """One libbre context on one GPU (mirrors the life of one PhotonBeamBVH + gather loop)."""
 
     def __init__(self, device: int = 0, counters: bool = False, timing: bool = False, kernel: int = 0,
-                 leaf_size: int | None = None, sqrt_mode: int = 0):
+                 leaf_size: int | None = None, sqrt_mode: int = 0, split: int | None = None,
+                 prefilter: bool | None = None):
         self.lib = load_library()
         h = ctypes.c_void_p()
         st = self.lib.bre_create(device, ctypes.byref(h))
@@ -131,6 +135,10 @@ class BeamGather:
         self.set_option(OPT_SQRT_MODE, sqrt_mode)
         if leaf_size is not None:
             self.set_option(OPT_LEAF_SIZE, leaf_size)
+        if split is not None:
+            self.set_option(OPT_SPLIT, split)
+        if prefilter is not None:
+            self.set_option(OPT_PREFILTER, int(prefilter))
         self._keep = []
 
     def _check(self, st):

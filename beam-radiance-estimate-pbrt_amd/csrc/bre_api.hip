@@ -53,6 +53,10 @@ struct bre_ctx {
     int kernel = 0;
     int leaf_size = 4;
     int sqrt_mode = 0;
+    int split = 8;
+    bool prefilter = true;
+    int debug_mode = 0;
+    int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     int built_leaf_size = 4;
@@ -61,7 +65,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf;
+    DevMem counters_buf, roots, partial;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bre_stats stats;
 };
@@ -97,6 +101,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nbeams = n;
     c->nvalid = 0;
     c->nnodes = 0;
+    c->roots_split = -1;
     c->stats = bre_stats{};
     c->stats.n_beams = n;
     if (n == 0) return BRE_OK;
@@ -201,14 +206,30 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.nvalid = c->nvalid;
     a.leaf_size = c->built_leaf_size;
     a.ctr = ctr;
+    a.split = c->split;
+    a.prefilter = c->prefilter;
+    a.debug_mode = c->debug_mode;
+    a.roots = nullptr;
+    a.partial = nullptr;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
         HIPCHK(c, launch_zero_outputs(a, c->stream));
         return BRE_OK;
     }
+    const int kernel = c->kernel == 2 ? 2 : 1;
+    if (kernel == 1) {
+        HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
+        HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)nseg * (size_t)c->split));
+        if (c->roots_split != c->split) {
+            HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
+            c->roots_split = c->split;
+        }
+        a.roots = c->roots.as<int32_t>();
+        a.partial = c->partial.as<float>();
+    }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-    HIPCHK(c, launch_gather(a, c->kernel == 2 ? 2 : 1, c->counters, c->stream));
+    HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
     if (c->timing || c->counters) {
         DevCounters h;
@@ -222,6 +243,11 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         c->stats.candidates = (int64_t)h.candidates;
         c->stats.contributions = (int64_t)h.contributions;
         c->stats.node_visits = (int64_t)h.node_visits;
+        c->stats.leaf_visits = (int64_t)h.leaf_visits;
+        c->stats.beam_evals = (int64_t)h.beam_evals;
+        c->stats.ccp_wave_evals = (int64_t)h.ccp_wave_evals;
+        c->stats.prefilter_rejects = (int64_t)h.prefilter_rejects;
+        c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
         if (h.flags & 1u) return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than stack)");
         if (h.flags & 2u) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix)");
     }
@@ -265,7 +291,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf};
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial};
     for (DevMem *m : all) m->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -292,6 +318,13 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SQRT_MODE must be 0 or 1");
         c->sqrt_mode = (int)value;
         return BRE_OK;
+    case BRE_OPT_SPLIT:
+        if (value < 1 || value > kMaxSplit || (value & (value - 1)))
+            return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SPLIT must be a power of two in 1..%d", kMaxSplit);
+        c->split = (int)value;
+        return BRE_OK;
+    case BRE_OPT_PREFILTER: c->prefilter = value != 0; return BRE_OK;
+    case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
 }

@@ -34,12 +34,18 @@ static_assert(sizeof(Node) == 64, "Node must be one 64-B line");
 constexpr int32_t kEmptyChild = INT32_MIN;
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
+constexpr int kMaxSplit = 64;          // max work roots (subtrees) per gather
 
 // Error / counter block in device memory (zeroed per call).
 struct DevCounters {
     unsigned long long candidates;
     unsigned long long contributions;
     unsigned long long node_visits;
+    unsigned long long leaf_visits;     // kernel 1: leaf clusters evaluated (per wave)
+    unsigned long long beam_evals;      // kernel 1: beam records evaluated (per wave)
+    unsigned long long ccp_wave_evals;  // kernel 1: exact closest-point executions (per wave)
+    unsigned long long prefilter_rejects;  // kernel 1: lane-level rejects by the line-distance filter
+    unsigned long long useful_beam_evals;  // kernel 1: beam evaluations with >= 1 lane passing the box
     unsigned int flags;  // bit0 stack overflow, bit1 pixel index out of range
     unsigned int pad;
 };
@@ -90,9 +96,16 @@ struct GatherArgs {
     int64_t nvalid;
     int leaf_size;
     DevCounters *ctr;
+    // wave kernel: subtree split
+    const int32_t *roots;  // [split] work roots + [split] = count
+    int split;             // S, power of two <= kMaxSplit
+    float *partial;        // [split][nseg][3]
+    bool prefilter;
+    int debug_mode;        // 0 normal; 1 timing-only: traversal without leaf evaluation
 };
 
 // gather kernels (bre_gather.hip)
+hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);
 hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStream_t s);
 hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s);
 

@@ -93,6 +93,9 @@ struct Box6 {
 };
 __host__ __device__ __forceinline__ bool slab_test(const Box6 &b, f3 o, f3 inv, int n0, int n1, int n2, float ray_tmax,
                                                    float *t_entry) {
+    // Branch-free statement of the reference's sequence: every step is computed and the early
+    // returns become a conjunction.  The `if (a > b) x = a` updates stay compare+select (not
+    // fmaxf/fminf) so NaNs from 0*inf propagate exactly as in the reference.
     const float pad = slab_pad();
     float tMin = ((n0 ? b.hx : b.lx) - o.x) * inv.x;
     float tMax = ((n0 ? b.lx : b.hx) - o.x) * inv.x;
@@ -100,17 +103,33 @@ __host__ __device__ __forceinline__ bool slab_test(const Box6 &b, f3 o, f3 inv, 
     float tyMax = ((n1 ? b.ly : b.hy) - o.y) * inv.y;
     tMax *= pad;
     tyMax *= pad;
-    if (tMin > tyMax || tyMin > tMax) return false;
-    if (tyMin > tMin) tMin = tyMin;
-    if (tyMax < tMax) tMax = tyMax;
+    const bool ok1 = !(tMin > tyMax || tyMin > tMax);
+    tMin = (tyMin > tMin) ? tyMin : tMin;
+    tMax = (tyMax < tMax) ? tyMax : tMax;
     const float tzMin = ((n2 ? b.hz : b.lz) - o.z) * inv.z;
     float tzMax = ((n2 ? b.lz : b.hz) - o.z) * inv.z;
     tzMax *= pad;
-    if (tMin > tzMax || tzMin > tMax) return false;
-    if (tzMin > tMin) tMin = tzMin;
-    if (tzMax < tMax) tMax = tzMax;
+    const bool ok2 = !(tMin > tzMax || tzMin > tMax);
+    tMin = (tzMin > tMin) ? tzMin : tMin;
+    tMax = (tzMax < tMax) ? tzMax : tMax;
     if (t_entry) *t_entry = tMin;
-    return (tMin < ray_tmax) && (tMax > 0);
+    return ok1 & ok2 & (tMin < ray_tmax) & (tMax > 0);
+}
+
+// The same decision for a NaN-free inverse direction (|inv| finite, nonzero: the sanitised one),
+// in min/max form: near/far per axis are min/max of the two plane distances (equal to the
+// reference's dirIsNeg selection when inv is finite), the pairwise overlap tests collapse to
+// max(near) <= min(far) (the self pairs hold whenever min(far) > 0), and the gamma(3) pad
+// commutes with min because rounding is monotone.  Bit-identical decision to slab_test(b, invs),
+// and monotone under box containment, so it is conservative for BVH interior (union) boxes.
+__host__ __device__ __forceinline__ bool node_test(const Box6 &b, f3 o, f3 invs, float ray_tmax, float &t_entry) {
+    const float ax = (b.lx - o.x) * invs.x, bx = (b.hx - o.x) * invs.x;
+    const float ay = (b.ly - o.y) * invs.y, by = (b.hy - o.y) * invs.y;
+    const float az = (b.lz - o.z) * invs.z, bz = (b.hz - o.z) * invs.z;
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * slab_pad();
+    t_entry = tn;
+    return (tn <= tf) & (tn < ray_tmax) & (tf > 0);
 }
 
 // ComputeClosestPoints, photonbeam.cpp:87-186, specialised to precomputed unit directions:

@@ -48,8 +48,13 @@ def parse():
     ap.add_argument("--radius", type=float, default=0.01)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=4)
+    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet (kernel 1)")
+    ap.add_argument("--prefilter", type=int, default=1)
+    ap.add_argument("--debug-mode", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
+                    help="camera: C2 primary segments (default, the metric); bounce: incoherent segments")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -78,13 +83,20 @@ def main():
     npix = frame.npix
     pixels = frame.pixels
     beams = synth.fog_beams(args.beams, seed=12345, radius=args.radius)
-    segs = synth.camera_segments(W, H, seed=777, pixels=pixels)
+    if args.segment_kind == "camera":
+        segs = synth.camera_segments(W, H, seed=777, pixels=pixels)
+    else:  # incoherent secondary segments, one per owned pixel
+        segs = synth.bounce_segments(len(pixels), seed=778 + rank)
+        segs["pixel"] = pixels.astype(np.int32)
     nseg = int(segs["tmax"].shape[0])
     dB = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in beams.items()}
     dS = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in segs.items()}
     accum = frame.accum
 
-    g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size)
+    g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
+                       prefilter=bool(args.prefilter))
+    if args.debug_mode:
+        g.set_option(100, args.debug_mode)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
@@ -164,6 +176,8 @@ def main():
             "parallelism": f"image-tiles x{world}, beams replicated",
             "kernel": "wave-packet" if args.kernel in (0, 1) else "thread-per-segment",
             "leaf_size": args.leaf_size,
+            "split": args.split,
+            "prefilter": bool(args.prefilter),
         },
         "gather_kernel_ms": gather_ms,
         "bvh_build_ms": st["build_ms"],
@@ -171,6 +185,11 @@ def main():
         "contributions_per_estimate": contrib_mean,
         "candidate_pair_tests_per_s": c_mean * value,
         "node_visits_per_wave": st["node_visits"] / max(waves, 1),
+        "leaf_visits_per_wave": st["leaf_visits"] / max(waves, 1),
+        "beam_evals_per_wave": st["beam_evals"] / max(waves, 1),
+        "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / max(waves, 1),
+        "useful_beam_evals_per_wave": st["useful_beam_evals"] / max(waves, 1),
+        "prefilter_rejects_per_estimate": st["prefilter_rejects"] / max(nseg, 1),
     }
 
     cpu = None

@@ -63,7 +63,10 @@ typedef enum bre_option {
     BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
     BRE_OPT_KERNEL = 3,      /* 0 = auto, 1 = wave-packet traversal, 2 = thread-per-segment */
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 4); applies at next build */
-    BRE_OPT_SQRT_MODE = 5    /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
+    BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
+    BRE_OPT_SPLIT = 6,       /* kernel 1: BVH subtrees per segment packet, power of two 1..64 (default 8) */
+    BRE_OPT_PREFILTER = 7    /* kernel 1: 0/1 conservative line-distance reject before the exact
+                                closest-point code (default 1; results are identical either way) */
 } bre_option;
 
 typedef struct bre_stats {
@@ -76,6 +79,11 @@ typedef struct bre_stats {
     int64_t contributions;   /* pairs with d < R + r that added to the pixel; counters only */
     int64_t node_visits;     /* interior-node visits summed over waves (kernel 1) or threads
                                 (kernel 2); counters only */
+    int64_t leaf_visits;     /* kernel 1, counters: leaf clusters evaluated, per wave */
+    int64_t beam_evals;      /* kernel 1, counters: beam records evaluated, per wave */
+    int64_t ccp_wave_evals;  /* kernel 1, counters: exact closest-point executions, per wave */
+    int64_t prefilter_rejects; /* kernel 1, counters: lane-level line-distance rejects */
+    int64_t useful_beam_evals; /* kernel 1, counters: beam evaluations where >= 1 lane is a candidate */
     double build_ms;         /* device time of the last BVH build (timing only) */
     double gather_ms;        /* device time of the last gather kernel (timing only) */
 } bre_stats;

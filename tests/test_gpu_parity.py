@@ -220,3 +220,37 @@ def test_deterministic_per_segment(bre, synth):
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
         b = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)["seg_rgb"]
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("split", [1, 2, 8, 64])
+def test_subtree_split_matches_oracle(bre, synth, oracle, split):
+    beams = synth.fog_beams(4000, seed=51)
+    segs = synth.camera_segments(40, 36, seed=52)
+    ref = oracle.build(beams).gather(segs, 0.01)
+    with bre.BeamGather(0, counters=True, kernel=1, split=split) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=0.01, counts=True)
+    assert np.array_equal(out["counts"][:, 0], ref["cand"])
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+@pytest.mark.parametrize("kind", ["camera", "bounce", "long"])
+def test_prefilter_changes_no_bit(bre, synth, kind):
+    """The conservative line-distance reject must not drop any contributing pair: outputs with and
+    without it are bit-identical, on coherent, incoherent and long-beam / large-radius inputs."""
+    if kind == "long":
+        beams = synth.fog_beams(6000, seed=61, radius=0.05, mean_length=0.8)
+        segs = synth.bounce_segments(6000, seed=62)
+        R = 0.08
+    else:
+        beams = synth.fog_beams(20000, seed=63)
+        segs = synth.camera_segments(64, 64, seed=64) if kind == "camera" else synth.bounce_segments(4096, seed=65)
+        R = 0.01
+    outs = []
+    for pf in (False, True):
+        with bre.BeamGather(0, counters=True, kernel=1, prefilter=pf) as g:
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True))
+    assert np.array_equal(outs[0]["seg_rgb"], outs[1]["seg_rgb"])
+    assert np.array_equal(outs[0]["counts"], outs[1]["counts"])
