@@ -46,6 +46,7 @@ class Stats(ctypes.Structure):
                 ("node_visits", ctypes.c_int64), ("leaf_visits", ctypes.c_int64),
                 ("beam_evals", ctypes.c_int64), ("ccp_wave_evals", ctypes.c_int64),
                 ("prefilter_rejects", ctypes.c_int64), ("useful_beam_evals", ctypes.c_int64),
+                ("max_stack_depth", ctypes.c_int64), ("redo_items", ctypes.c_int64),
                 ("build_ms", ctypes.c_double),
                 ("gather_ms", ctypes.c_double)]
 

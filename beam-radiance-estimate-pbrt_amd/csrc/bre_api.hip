@@ -51,21 +51,23 @@ struct bre_ctx {
     bool counters = false;
     bool timing = false;
     int kernel = 0;
-    int leaf_size = 4;
+    int leaf_size = 1;
     int sqrt_mode = 0;
-    int split = 8;
+    int split = 16;
     bool prefilter = true;
     int debug_mode = 0;
+    int stack_limit = 0;
+    int occupancy = 0;
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
-    int built_leaf_size = 4;
+    int built_leaf_size = 1;
     DevMem in_start, in_end, in_radius, in_power;  // staging for host-pointer uploads
     DevMem box, cent, cbounds, nvalid_buf, keys, keys_alt, vals, vals_alt, sort_tmp, leaf_parent, visit;
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial;
+    DevMem counters_buf, roots, partial, pcnt, redo;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bre_stats stats;
 };
@@ -209,16 +211,25 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.split = c->split;
     a.prefilter = c->prefilter;
     a.debug_mode = c->debug_mode;
+    a.stack_limit = c->stack_limit;
+    a.occupancy = c->occupancy;
     a.roots = nullptr;
     a.partial = nullptr;
+    a.pcnt = nullptr;
+    a.redo = nullptr;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
         HIPCHK(c, launch_zero_outputs(a, c->stream));
         return BRE_OK;
     }
-    const int kernel = c->kernel == 2 ? 2 : 1;
-    if (kernel == 1) {
+    // auto (0): the packet-proxy kernel 3 (with kernel 1 as its device-side overflow fallback)
+    // when leaf clusters are small enough for its candidate list, else kernel 1
+    int kernel = c->kernel;
+    if (kernel == 0) kernel = c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 1;
+    if (kernel == 3 && c->built_leaf_size > kProxyMaxLeafHost)
+        return fail(c, BRE_ERR_STATE, "kernel 3 needs BRE_OPT_LEAF_SIZE <= %d", kProxyMaxLeafHost);
+    if (kernel != 2) {
         HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
         HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)nseg * (size_t)c->split));
         if (c->roots_split != c->split) {
@@ -227,6 +238,12 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         a.roots = c->roots.as<int32_t>();
         a.partial = c->partial.as<float>();
+        HIPCHK(c, c->redo.ensure((size_t)(nseg + 63) / 64 + 16));
+        a.redo = c->redo.as<uint8_t>();
+        if (c->counters) {
+            HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
+            a.pcnt = c->pcnt.as<int32_t>();
+        }
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
@@ -248,6 +265,8 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         c->stats.ccp_wave_evals = (int64_t)h.ccp_wave_evals;
         c->stats.prefilter_rejects = (int64_t)h.prefilter_rejects;
         c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
+        c->stats.max_stack_depth = (int64_t)h.max_stack;
+        c->stats.redo_items = (int64_t)h.redo_items;
         if (h.flags & 1u) return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than stack)");
         if (h.flags & 2u) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix)");
     }
@@ -291,7 +310,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial};
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo};
     for (DevMem *m : all) m->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -307,7 +326,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
     case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
     case BRE_OPT_KERNEL:
-        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..3");
         c->kernel = (int)value;
         return BRE_OK;
     case BRE_OPT_LEAF_SIZE:
@@ -325,6 +344,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         return BRE_OK;
     case BRE_OPT_PREFILTER: c->prefilter = value != 0; return BRE_OK;
     case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
+    case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
+    case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 3 register budget
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
 }

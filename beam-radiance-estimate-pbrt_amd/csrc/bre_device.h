@@ -35,6 +35,7 @@ constexpr int32_t kEmptyChild = INT32_MIN;
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
 constexpr int kMaxSplit = 64;          // max work roots (subtrees) per gather
+constexpr int kProxyMaxLeafHost = 4;   // kernel 3 candidate list sized for leaf clusters <= 4
 
 // Error / counter block in device memory (zeroed per call).
 struct DevCounters {
@@ -46,8 +47,9 @@ struct DevCounters {
     unsigned long long ccp_wave_evals;  // kernel 1: exact closest-point executions (per wave)
     unsigned long long prefilter_rejects;  // kernel 1: lane-level rejects by the line-distance filter
     unsigned long long useful_beam_evals;  // kernel 1: beam evaluations with >= 1 lane passing the box
-    unsigned int flags;  // bit0 stack overflow, bit1 pixel index out of range
-    unsigned int pad;
+    unsigned long long redo_items;         // kernel 3: (packet, subtree) items handed to kernel 1
+    unsigned int flags;  // bit0 stack overflow, bit1 pixel index out of range, bit2 proxy-stack overflow
+    unsigned int max_stack;  // kernel 3: deepest LDS node stack seen
 };
 
 struct BuildBuffers {
@@ -100,8 +102,12 @@ struct GatherArgs {
     const int32_t *roots;  // [split] work roots + [split] = count
     int split;             // S, power of two <= kMaxSplit
     float *partial;        // [split][nseg][3]
+    int32_t *pcnt;         // [split][nseg][2] per-subtree counts (counters only)
     bool prefilter;
     int debug_mode;        // 0 normal; 1 timing-only: traversal without leaf evaluation
+    int stack_limit;       // kernel 3 LDS stack entries to use (0 = all); tests force the fallback
+    int occupancy;         // kernel 3 register budget: min waves per SIMD (1, 6 or 8)
+    uint8_t *redo;         // kernel 3: [packets] flags of packets handed to kernel 1
 };
 
 // gather kernels (bre_gather.hip)

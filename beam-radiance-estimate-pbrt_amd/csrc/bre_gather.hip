@@ -49,6 +49,7 @@ struct BeamV {
     Box6 box;
     f3 b0, bu;
     float mag_b, radius;
+    f3 pw;  // scaled powerEnd, when the caller already has it (kernel 3 batches)
 };
 __device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int64_t i) {
     const float4 *q = reinterpret_cast<const float4 *>(recs + i);
@@ -59,11 +60,12 @@ __device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int
     r.bu = mk(z.y, z.z, z.w);
     r.mag_b = w.x;
     r.radius = w.y;
+    r.pw = mk(0.f, 0.f, 0.f);
     return r;
 }
 
 struct Lane {
-    f3 o, p, au;
+    f3 o, p, au, d;
     f3 inv, invs;
     float tmax, mag_a;
     float omax;  // max |o_i| + |A|: bounds the segment-side coordinates (prefilter margin)
@@ -79,7 +81,7 @@ __device__ __forceinline__ bool load_lane(int64_t s, int64_t nseg, const float *
                                           const float *__restrict__ p, const float *__restrict__ d,
                                           const float *__restrict__ tmax, Lane &L) {
     if (s >= nseg) {
-        L.o = L.p = L.au = L.inv = L.invs = mk(0.f, 0.f, 0.f);
+        L.o = L.p = L.au = L.d = L.inv = L.invs = mk(0.f, 0.f, 0.f);
         L.tmax = 0.f;
         L.mag_a = 0.f;
         L.omax = 0.f;
@@ -90,11 +92,12 @@ __device__ __forceinline__ bool load_lane(int64_t s, int64_t nseg, const float *
     L.o = mk(o[3 * s], o[3 * s + 1], o[3 * s + 2]);
     L.p = mk(p[3 * s], p[3 * s + 1], p[3 * s + 2]);
     const f3 dd = mk(d[3 * s], d[3 * s + 1], d[3 * s + 2]);
+    L.d = dd;
     L.tmax = tmax[s];
     // invDir(1 / ray.d.x, ...), dirIsNeg = invDir < 0  (photonbeambvh.cpp:690-691)
     L.inv = mk(1 / dd.x, 1 / dd.y, 1 / dd.z);
     L.invs = mk(sanitize_inv(L.inv.x), sanitize_inv(L.inv.y), sanitize_inv(L.inv.z));
-    L.has_inf = isinf(L.inv.x) | isinf(L.inv.y) | isinf(L.inv.z);
+    L.has_inf = isinf(L.inv.x) || isinf(L.inv.y) || isinf(L.inv.z);
     L.n0 = L.inv.x < 0;
     L.n1 = L.inv.y < 0;
     L.n2 = L.inv.z < 0;
@@ -134,7 +137,7 @@ struct Prof {
     unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0;
 };
 
-template <bool COUNT, bool PREF>
+template <bool COUNT, bool PREF, bool PWREG = false>
 __device__ __forceinline__ void eval_beam(const Lane &L, bool lane_on, const BeamV &r, const float4 *__restrict__ pw,
                                           int64_t bi, float R, float &cr, float &cg, float &cb, int &cand,
                                           int &contrib, Prof &pf, int dbg = 0) {
@@ -168,10 +171,20 @@ __device__ __forceinline__ void eval_beam(const Lane &L, bool lane_on, const Bea
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
             const float w = sqrtf(1.0f - rr * rr);
-            const float4 pv = pw[bi];
-            cr += pv.x * w;
-            cg += pv.y * w;
-            cb += pv.z * w;
+            float px, py, pz;
+            if (PWREG) {
+                px = r.pw.x;
+                py = r.pw.y;
+                pz = r.pw.z;
+            } else {
+                const float4 pv = pw[bi];
+                px = pv.x;
+                py = pv.y;
+                pz = pv.z;
+            }
+            cr += px * w;
+            cg += py * w;
+            cb += pz * w;
             if (COUNT) ++contrib;
         }
     }
@@ -221,6 +234,99 @@ __device__ __forceinline__ void finish_lane(int64_t s, bool valid, float cr, flo
     }
 }
 
+// Depth-first wave-packet traversal of one work root (kernel 1, and kernel 3's path for loose
+// packets): the current node and the stack are wave-uniform, node and beam lines are SMEM loads,
+// each lane tests both children with node_test and the descent is a ballot.
+template <bool COUNT, bool PREF>
+__device__ __forceinline__ void dfs_packet(const Lane &L, bool valid, int32_t root, int32_t *stk,
+                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                           const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, float R,
+                                           float &cr, float &cg, float &cb, int &cand, int &contrib,
+                                           unsigned long long &visits, Prof &pf, DevCounters *ctr, int dbg) {
+    if (root < 0) {
+        // the work root is a leaf cluster: evaluate it directly
+        const int64_t first = (int64_t)(~root) * leaf_size;
+        const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+        if (COUNT) {
+            ++pf.leaves;
+            pf.beams += cnt;
+        }
+        for (int j = 0; j < cnt; ++j)
+            eval_beam<COUNT, PREF>(L, valid, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
+                                   contrib, pf, dbg);
+    } else {
+        int node = root;
+        int sp = 0;
+        while (true) {
+            node = __builtin_amdgcn_readfirstlane(node);
+            const NodeV n = load_node(nodes, node);
+            if (COUNT) ++visits;
+            const int32_t c0 = n.c0, c1 = n.c1;
+            float te0 = 0.f, te1 = 0.f;
+            const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, L.o, L.invs, L.tmax, te0);
+            const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, L.o, L.invs, L.tmax, te1);
+            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+            // leaves are evaluated in place
+            bool go0 = m0 != 0ull, go1 = m1 != 0ull;
+            if (dbg == 1) {  // timing-only build: traversal without leaf work
+                if (go0 && c0 < 0) go0 = false;
+                if (go1 && c1 < 0) go1 = false;
+            }
+            if (go0 && c0 < 0) {
+                const int64_t first = (int64_t)(~c0) * leaf_size;
+                const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+                if (COUNT) {
+                    ++pf.leaves;
+                    pf.beams += cnt;
+                }
+                for (int j = 0; j < cnt; ++j)
+                    eval_beam<COUNT, PREF>(L, h0, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
+                                           contrib, pf, dbg);
+                go0 = false;
+            }
+            if (go1 && c1 < 0) {
+                const int64_t first = (int64_t)(~c1) * leaf_size;
+                const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+                if (COUNT) {
+                    ++pf.leaves;
+                    pf.beams += cnt;
+                }
+                for (int j = 0; j < cnt; ++j)
+                    eval_beam<COUNT, PREF>(L, h1, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
+                                           contrib, pf, dbg);
+                go1 = false;
+            }
+            if (go0 && go1) {
+                // near child first, judged by the first lane that enters both
+                const unsigned long long both = m0 & m1;
+                bool first0 = true;
+                if (both != 0ull) {
+                    const int fl = __ffsll((long long)both) - 1;
+                    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
+                    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
+                    first0 = !(b < a);
+                }
+                const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
+                if (sp >= kStackDepth) {
+                    if ((threadIdx.x & 63) == 0) atomicOr(&ctr->flags, 1u);
+                    break;
+                }
+                stk[sp] = far;  // every lane writes the same value
+                ++sp;
+                node = near;
+            } else if (go0) {
+                node = c0;
+            } else if (go1) {
+                node = c1;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp];
+            }
+        }
+    }
+}
+
 // Wave-packet traversal of one BVH subtree.  Grid = (segment groups of 256) x S subtrees with
 // subtree = blockIdx % S: the S work roots partition the beams, so every (packet, subtree) pair is
 // an independent work item (8x the waves of one full traversal per packet: load balance and latency
@@ -230,9 +336,10 @@ __device__ __forceinline__ void finish_lane(int64_t s, bool valid, float cr, flo
 template <bool COUNT, bool PREF>
 __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
-    const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ seg_counts,
+    const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
     const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
-    int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int dbg) {
+    int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int dbg,
+    const uint8_t *__restrict__ redo) {
     __shared__ int32_t stk[kWaveBlock / 64][kStackDepth];
     // Block -> (subtree, packet group).  Blocks b and b+8 share an XCD under the observed
     // round-robin dispatch, so for S >= 8 XCD (b & 7) is given the S/8 consecutive work roots
@@ -251,6 +358,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
     if (sub >= roots[S]) return;  // fewer work roots than S (small trees): whole block exits
     const int w = threadIdx.x >> 6;
     const int64_t s = grp * kWaveBlock + threadIdx.x;
+    // behind kernel 3, only the packets it handed over (incoherent, or out of LDS stack) run here
+    if (redo && (s >= nseg || !redo[s >> 6])) return;  // per wave: all lanes share the packet
     Lane L;
     const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
     float cr = 0.f, cg = 0.f, cb = 0.f;
@@ -259,98 +368,17 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
     Prof pf;
 
     if (__ballot(valid) != 0ull) {
-        const int32_t root = roots[sub];
-        if (root < 0) {
-            // the work root is a leaf cluster: evaluate it directly
-            const int64_t first = (int64_t)(~root) * leaf_size;
-            const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
-            if (COUNT) {
-                ++pf.leaves;
-                pf.beams += cnt;
-            }
-            for (int j = 0; j < cnt; ++j)
-                eval_beam<COUNT, PREF>(L, valid, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
-                                       contrib, pf, dbg);
-        } else {
-            int node = root;
-            int sp = 0;
-            while (true) {
-                node = __builtin_amdgcn_readfirstlane(node);
-                const NodeV n = load_node(nodes, node);
-                if (COUNT) ++visits;
-                const int32_t c0 = n.c0, c1 = n.c1;
-                float te0 = 0.f, te1 = 0.f;
-                const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, L.o, L.invs, L.tmax, te0);
-                const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, L.o, L.invs, L.tmax, te1);
-                const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-                // leaves are evaluated in place
-                bool go0 = m0 != 0ull, go1 = m1 != 0ull;
-                if (dbg == 1) {  // timing-only build: traversal without leaf work
-                    if (go0 && c0 < 0) go0 = false;
-                    if (go1 && c1 < 0) go1 = false;
-                }
-                if (go0 && c0 < 0) {
-                    const int64_t first = (int64_t)(~c0) * leaf_size;
-                    const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
-                    if (COUNT) {
-                        ++pf.leaves;
-                        pf.beams += cnt;
-                    }
-                    for (int j = 0; j < cnt; ++j)
-                        eval_beam<COUNT, PREF>(L, h0, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
-                                               contrib, pf, dbg);
-                    go0 = false;
-                }
-                if (go1 && c1 < 0) {
-                    const int64_t first = (int64_t)(~c1) * leaf_size;
-                    const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
-                    if (COUNT) {
-                        ++pf.leaves;
-                        pf.beams += cnt;
-                    }
-                    for (int j = 0; j < cnt; ++j)
-                        eval_beam<COUNT, PREF>(L, h1, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand,
-                                               contrib, pf, dbg);
-                    go1 = false;
-                }
-                if (go0 && go1) {
-                    // near child first, judged by the first lane that enters both
-                    const unsigned long long both = m0 & m1;
-                    bool first0 = true;
-                    if (both != 0ull) {
-                        const int fl = __ffsll((long long)both) - 1;
-                        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
-                        const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
-                        first0 = !(b < a);
-                    }
-                    const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
-                    if (sp >= kStackDepth) {
-                        if ((threadIdx.x & 63) == 0) atomicOr(&ctr->flags, 1u);
-                        break;
-                    }
-                    stk[w][sp] = far;  // every lane writes the same value
-                    ++sp;
-                    node = near;
-                } else if (go0) {
-                    node = c0;
-                } else if (go1) {
-                    node = c1;
-                } else {
-                    if (sp == 0) break;
-                    --sp;
-                    node = stk[w][sp];
-                }
-            }
-        }
+        dfs_packet<COUNT, PREF>(L, valid, roots[sub], stk[w], recs, pw, nodes, nvalid, leaf_size, R, cr, cg, cb, cand,
+                                contrib, visits, pf, ctr, dbg);
     }
     if (valid) {
         float *dst = partial + 3 * ((int64_t)sub * nseg + s);
         dst[0] = cr;
         dst[1] = cg;
         dst[2] = cb;
-        if (COUNT && seg_counts) {
-            atomicAdd(&seg_counts[2 * s], cand);
-            atomicAdd(&seg_counts[2 * s + 1], contrib);
+        if (COUNT) {
+            pcnt[2 * ((int64_t)sub * nseg + s)] = cand;
+            pcnt[2 * ((int64_t)sub * nseg + s) + 1] = contrib;
         }
     }
     if (COUNT) {
@@ -364,9 +392,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
         unsigned long long rj = pf.rejects;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) rj += __shfl_xor(rj, off);
+        (void)c;
+        (void)k;
         if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&ctr->candidates, c);
-            atomicAdd(&ctr->contributions, k);
             atomicAdd(&ctr->node_visits, visits);
             atomicAdd(&ctr->leaf_visits, pf.leaves);
             atomicAdd(&ctr->beam_evals, pf.beams);
@@ -381,36 +409,361 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Kernel 3 (k_gather_proxy): packet-proxy traversal.  A wave owns one packet of 64 coherent
+// segments and one BVH work root.  Instead of walking the tree node by node with all 64 lanes
+// testing the same node (kernel 1), each lane takes a DIFFERENT node from a wave-shared LDS stack
+// and tests its two children against a conservative proxy of the whole packet (interval slab test
+// over the packet's origin box x inverse-direction box, plus the packet's segment AABB): 64 nodes
+// per step, one vector load per lane, no dependent per-node latency.  Hit leaves append their beams
+// to an LDS candidate list; every 64 candidates are loaded with one vector load per lane and
+// broadcast one by one (v_readlane) to all lanes, which run the exact reference tests per lane.
+//
+// Conservativeness chain (why no candidate is lost): a lane's exact slab hit on a beam box =>
+// node_test on that box (bre_math.h) => node_test on every ancestor (monotone under containment)
+// => proxy_test on every ancestor (the lane's float values (b - o)*v lie between the corner values
+// the proxy computes with the same float operations, because rounding is monotone and the
+// function is bilinear).  The proxy only decides WHICH beams get the exact per-lane test.
+constexpr int kProxyStack = 1024;  // LDS node-stack entries per wave (>= kStackDepth: reused by dfs); 550 seen at C2
+constexpr float kLooseCos = 0.9976f;  // packets whose directions spread > ~4 deg use the dfs path
+constexpr int kProxyMaxLeaf = 4;             // kernel 3 needs leaf clusters of <= 4 beams
+constexpr int kCandCap = 64 + 2 * 64 * kProxyMaxLeaf;  // leftover + one step's leaf beams
+
+struct Proxy {
+    float olo[3], ohi[3];   // packet origin box
+    float ilo[3], ihi[3];   // packet box of sanitised 1/d
+    int sgn[3];             // +1 / -1 if every lane's 1/d_i has that sign, 0 if mixed
+    float alo[3], ahi[3];   // AABB of all segments [o, o + tmax*d], padded
+    float tmax;             // max ray.tMax
+};
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+
+__device__ __forceinline__ Proxy make_proxy(const Lane &L, bool valid) {
+    Proxy P;
+    const float o[3] = {L.o.x, L.o.y, L.o.z};
+    const float iv[3] = {L.invs.x, L.invs.y, L.invs.z};
+    const float dd[3] = {L.d.x, L.d.y, L.d.z};
+    float mag = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) mag = fmaxf(mag, fabsf(o[k]) + L.tmax * fabsf(dd[k]));
+    const float pad = 1e-5f * mag + 1e-6f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float e = o[k] + L.tmax * dd[k];
+        P.olo[k] = wave_min(valid ? o[k] : FLT_MAX);
+        P.ohi[k] = wave_max(valid ? o[k] : -FLT_MAX);
+        P.ilo[k] = wave_min(valid ? iv[k] : FLT_MAX);
+        P.ihi[k] = wave_max(valid ? iv[k] : -FLT_MAX);
+        P.alo[k] = wave_min(valid ? fminf(o[k], e) - pad : FLT_MAX);
+        P.ahi[k] = wave_max(valid ? fmaxf(o[k], e) + pad : -FLT_MAX);
+        P.sgn[k] = (P.ilo[k] > 0.f) ? 1 : ((P.ihi[k] < 0.f) ? -1 : 0);
+    }
+    P.tmax = wave_max(valid ? L.tmax : -FLT_MAX);
+    return P;
+}
+
+__device__ __forceinline__ float min4(float a, float b, float c, float d) { return fminf(fminf(a, b), fminf(c, d)); }
+__device__ __forceinline__ float max4(float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); }
+
+__device__ __forceinline__ bool proxy_test(const Proxy &P, const Box6 &b) {
+    const float lo[3] = {b.lx, b.ly, b.lz}, hi[3] = {b.hx, b.hy, b.hz};
+    bool ok = true;
+    float tn = -FLT_MAX, tf = FLT_MAX;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        ok = ok & (hi[k] >= P.alo[k]) & (lo[k] <= P.ahi[k]);
+        if (P.sgn[k] != 0) {  // wave-uniform
+            const float bn = P.sgn[k] > 0 ? lo[k] : hi[k];
+            const float bf = P.sgn[k] > 0 ? hi[k] : lo[k];
+            const float n0 = bn - P.olo[k], n1 = bn - P.ohi[k];
+            const float f0 = bf - P.olo[k], f1 = bf - P.ohi[k];
+            tn = fmaxf(tn, min4(n0 * P.ilo[k], n0 * P.ihi[k], n1 * P.ilo[k], n1 * P.ihi[k]));
+            tf = fminf(tf, max4(f0 * P.ilo[k], f0 * P.ihi[k], f1 * P.ilo[k], f1 * P.ihi[k]));
+        }
+    }
+    tf = tf * slab_pad();
+    return ok & (tn <= tf) & (tn < P.tmax) & (tf > 0.f);
+}
+
+// exclusive prefix sum of a small non-negative int over the wave
+__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    total = __shfl(x, 63);
+    return x - v;
+}
+
+template <bool COUNT, bool PREF>
+__device__ __forceinline__ void proxy_batch(const Lane &L, bool valid, const int32_t *cand, int nb,
+                                            const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                            float R, float &cr, float &cg, float &cb, int &ccount, int &contrib,
+                                            Prof &pf, int dbg) {
+    const int lane = threadIdx.x & 63;
+    int bi = 0;
+    BeamV mine;
+    float4 mpw = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < nb) {
+        bi = cand[lane];
+        mine = load_beam(recs, bi);
+        mpw = pw[bi];
+    } else {
+        mine = BeamV{};
+    }
+    if (COUNT) pf.beams += nb;
+    for (int j = 0; j < nb; ++j) {
+        BeamV r;
+        const auto rl = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)); };
+        r.box = Box6{rl(mine.box.lx), rl(mine.box.ly), rl(mine.box.lz), rl(mine.box.hx), rl(mine.box.hy),
+                     rl(mine.box.hz)};
+        r.b0 = mk(rl(mine.b0.x), rl(mine.b0.y), rl(mine.b0.z));
+        r.bu = mk(rl(mine.bu.x), rl(mine.bu.y), rl(mine.bu.z));
+        r.mag_b = rl(mine.mag_b);
+        r.radius = rl(mine.radius);
+        r.pw = mk(rl(mpw.x), rl(mpw.y), rl(mpw.z));
+        eval_beam<COUNT, PREF, true>(L, valid, r, pw, 0, R, cr, cg, cb, ccount, contrib, pf, dbg);
+    }
+}
+
+template <bool COUNT, bool PREF, int MINW>
+__global__ __launch_bounds__(64, MINW) void k_gather_proxy(
+    int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
+    const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
+    const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
+    int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int stack_limit, int dbg,
+    uint8_t *__restrict__ redo) {
+    __shared__ int32_t stk[kProxyStack];
+    __shared__ int32_t cand[kCandCap];
+    int sub;
+    int64_t grp;
+    if (S >= 8) {
+        const unsigned per = (unsigned)S >> 3;
+        const unsigned q = blockIdx.x >> 3;
+        sub = (int)((blockIdx.x & 7u) * per + q % per);
+        grp = q / per;
+    } else {
+        sub = (int)(blockIdx.x % (unsigned)S);
+        grp = blockIdx.x / (unsigned)S;
+    }
+    if (sub >= roots[S]) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = grp * 64 + lane;
+    Lane L;
+    const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
+    float cr = 0.f, cg = 0.f, cb = 0.f;
+    int ccount = 0, contrib = 0;
+    Prof pf;
+    unsigned long long tests = 0;
+    int maxsp = 0;
+    bool overflow = false;
+
+    // Incoherent packets (directions spread wider than kLooseCos) make the proxy useless: they take
+    // the depth-first per-lane path instead (kernel 1's traversal, same exact per-lane tests).
+    bool loose = false;
+    if (__ballot(valid) != 0ull) {
+        float sx = valid ? L.d.x : 0.f, sy = valid ? L.d.y : 0.f, sz = valid ? L.d.z : 0.f;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            sx += __shfl_xor(sx, off);
+            sy += __shfl_xor(sy, off);
+            sz += __shfl_xor(sz, off);
+        }
+        const float sn = sqrtf(sx * sx + sy * sy + sz * sz);
+        const float dn = sqrtf(lensq3(L.d));
+        const float c = (valid && sn > 0.f && dn > 0.f) ? (sx * L.d.x + sy * L.d.y + sz * L.d.z) / (sn * dn) : 1.0f;
+        loose = wave_min(c) < kLooseCos;
+    }
+    if (loose) {
+        // handed to kernel 1 (depth-first per-lane traversal), which runs behind this launch
+    } else if (__ballot(valid) != 0ull) {
+        const Proxy P = make_proxy(L, valid);
+        const int32_t root = roots[sub];
+        int sp = 0, nc = 0;
+        if (root < 0) {
+            const int64_t first = (int64_t)(~root) * leaf_size;
+            const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+            if (lane < cnt) cand[lane] = (int32_t)(first + lane);
+            nc = cnt;
+        } else {
+            if (lane == 0) stk[0] = root;
+            sp = 1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        while (sp > 0 || nc > 0) {
+            if (sp > 0) {
+                int n = min(64, sp);
+                if (sp + n > stack_limit) n = stack_limit - sp;
+                if (n <= 0) {
+                    overflow = true;
+                    break;
+                }
+                const int base = sp - n;
+                int32_t node = 0;
+                if (lane < n) node = stk[base + lane];
+                __builtin_amdgcn_wave_barrier();
+                sp = base;
+                bool h0 = false, h1 = false;
+                int32_t c0 = kEmptyChild, c1 = kEmptyChild;
+                if (lane < n) {
+                    const NodeV nd = load_node(nodes, node);
+                    c0 = nd.c0;
+                    c1 = nd.c1;
+                    h0 = (c0 != kEmptyChild) && proxy_test(P, nd.b0);
+                    h1 = (c1 != kEmptyChild) && proxy_test(P, nd.b1);
+                }
+                if (COUNT) tests += n;
+                // push interior children
+                const bool p0 = h0 && c0 >= 0, p1 = h1 && c1 >= 0;
+                int tot;
+                const int pos = wave_excl_scan((int)p0 + (int)p1, tot);
+                if (p0) stk[sp + pos] = c0;
+                if (p1) stk[sp + pos + (int)p0] = c1;
+                sp += tot;
+                // append leaf beams
+                int k0 = 0, k1 = 0;
+                int64_t f0 = 0, f1 = 0;
+                if (h0 && c0 < 0) {
+                    f0 = (int64_t)(~c0) * leaf_size;
+                    k0 = (int)min((int64_t)leaf_size, nvalid - f0);
+                }
+                if (h1 && c1 < 0) {
+                    f1 = (int64_t)(~c1) * leaf_size;
+                    k1 = (int)min((int64_t)leaf_size, nvalid - f1);
+                }
+                int ltot;
+                const int lpos = wave_excl_scan(k0 + k1, ltot);
+                for (int j = 0; j < k0; ++j) cand[nc + lpos + j] = (int32_t)(f0 + j);
+                for (int j = 0; j < k1; ++j) cand[nc + lpos + k0 + j] = (int32_t)(f1 + j);
+                nc += ltot;
+                if (COUNT) {
+                    pf.leaves += __popcll(__ballot(k0 > 0)) + __popcll(__ballot(k1 > 0));
+                    maxsp = max(maxsp, sp);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            // evaluate full batches (and the remainder once the stack is empty)
+            while (nc >= 64 || (sp == 0 && nc > 0)) {
+                const int nb = min(64, nc);
+                nc -= nb;
+                if (dbg != 1)  // dbg 1: timing-only traversal
+                    proxy_batch<COUNT, PREF>(L, valid, cand + nc, nb, recs, pw, R, cr, cg, cb, ccount, contrib, pf,
+                                             dbg);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    if (loose || overflow) {
+        // kernel 1 redoes this packet for every subtree; nothing of this wave is kept
+        if (lane == 0) {
+            redo[grp] = 1;
+            if (COUNT) atomicAdd(&ctr->redo_items, 1ull);
+        }
+        return;
+    }
+    if (valid) {
+        float *dst = partial + 3 * ((int64_t)sub * nseg + s);
+        dst[0] = cr;
+        dst[1] = cg;
+        dst[2] = cb;
+        if (COUNT) {
+            pcnt[2 * ((int64_t)sub * nseg + s)] = ccount;
+            pcnt[2 * ((int64_t)sub * nseg + s) + 1] = contrib;
+        }
+    }
+    if (COUNT) {
+        unsigned long long c = valid ? (unsigned long long)ccount : 0ull;
+        unsigned long long k = valid ? (unsigned long long)contrib : 0ull;
+        unsigned long long rj = pf.rejects, cw = pf.ccp_waves;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            c += __shfl_xor(c, off);
+            k += __shfl_xor(k, off);
+            rj += __shfl_xor(rj, off);
+            cw += __shfl_xor(cw, off);
+        }
+        (void)c;
+        (void)k;
+        if (lane == 0) {
+            atomicAdd(&ctr->node_visits, tests);
+            atomicAdd(&ctr->leaf_visits, pf.leaves);
+            atomicAdd(&ctr->beam_evals, pf.beams);
+            atomicAdd(&ctr->useful_beam_evals, pf.useful);
+            atomicAdd(&ctr->prefilter_rejects, rj);
+            atomicAdd(&ctr->ccp_wave_evals, cw);
+            atomicMax(&ctr->max_stack, (unsigned int)maxsp);
+        }
+    }
+}
+
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the
-// segment's sum to its pixel (one float atomic per channel, PhotonBeamPixel::Ld +=).
+// segment's sum to its pixel (one float atomic per channel, PhotonBeamPixel::Ld +=).  With
+// counters, also sum the per-subtree candidate / contribution counts.
 __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__restrict__ partial,
-                                                const int32_t *__restrict__ roots, int S,
-                                                const int32_t *__restrict__ pixel, int64_t npix,
+                                                const int32_t *__restrict__ pcnt, const int32_t *__restrict__ roots,
+                                                int S, const int32_t *__restrict__ pixel, int64_t npix,
                                                 float *__restrict__ accum, float *__restrict__ seg_rgb,
-                                                DevCounters *ctr) {
+                                                int32_t *__restrict__ seg_counts, DevCounters *ctr) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= nseg) return;
+    const bool in = s < nseg;
     const int nr = roots[S];
     float cr = 0.f, cg = 0.f, cb = 0.f;
-    for (int k = 0; k < nr; ++k) {
-        const float *q = partial + 3 * ((int64_t)k * nseg + s);
-        cr += q[0];
-        cg += q[1];
-        cb += q[2];
+    long long c = 0, k = 0;
+    if (in) {
+        for (int j = 0; j < nr; ++j) {
+            const float *q = partial + 3 * ((int64_t)j * nseg + s);
+            cr += q[0];
+            cg += q[1];
+            cb += q[2];
+            if (pcnt) {
+                c += pcnt[2 * ((int64_t)j * nseg + s)];
+                k += pcnt[2 * ((int64_t)j * nseg + s) + 1];
+            }
+        }
+        if (seg_rgb) {
+            seg_rgb[3 * s] = cr;
+            seg_rgb[3 * s + 1] = cg;
+            seg_rgb[3 * s + 2] = cb;
+        }
+        if (seg_counts) {
+            seg_counts[2 * s] = (int32_t)c;
+            seg_counts[2 * s + 1] = (int32_t)k;
+        }
+        if (accum) {
+            const int32_t px = pixel[s];
+            if (px < 0 || px >= npix) {
+                atomicOr(&ctr->flags, 2u);
+            } else if (cr != 0.f || cg != 0.f || cb != 0.f) {
+                atomicAdd(&accum[3 * (int64_t)px], cr);
+                atomicAdd(&accum[3 * (int64_t)px + 1], cg);
+                atomicAdd(&accum[3 * (int64_t)px + 2], cb);
+            }
+        }
     }
-    if (seg_rgb) {
-        seg_rgb[3 * s] = cr;
-        seg_rgb[3 * s + 1] = cg;
-        seg_rgb[3 * s + 2] = cb;
-    }
-    if (accum) {
-        const int32_t px = pixel[s];
-        if (px < 0 || px >= npix) {
-            atomicOr(&ctr->flags, 2u);
-        } else if (cr != 0.f || cg != 0.f || cb != 0.f) {
-            atomicAdd(&accum[3 * (int64_t)px], cr);
-            atomicAdd(&accum[3 * (int64_t)px + 1], cg);
-            atomicAdd(&accum[3 * (int64_t)px + 2], cb);
+    if (pcnt) {
+        unsigned long long uc = (unsigned long long)c, uk = (unsigned long long)k;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            uc += __shfl_xor(uc, off);
+            uk += __shfl_xor(uk, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&ctr->candidates, uc);
+            atomicAdd(&ctr->contributions, uk);
         }
     }
 }
@@ -547,16 +900,36 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
                                a.nvalid, a.leaf_size, a.ctr);
         return hipGetLastError();
     }
-    if (counters && a.seg_counts) {
-        hipError_t e = hipMemsetAsync(a.seg_counts, 0, sizeof(int32_t) * 2 * (size_t)a.nseg, s);
-        if (e != hipSuccess) return e;
+    if (kernel == 3) {
+        const int64_t packets = (a.nseg + 63) / 64;
+        hipError_t em = hipMemsetAsync(a.redo, 0, (size_t)packets, s);
+        if (em != hipSuccess) return em;
+        const dim3 grid3((unsigned int)(packets * a.split));
+#define BRE_LAUNCH_PROXY_W(C, P, W)                                                                              \
+    hipLaunchKernelGGL((k_gather_proxy<C, P, W>), grid3, dim3(64), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R,      \
+                       a.partial, a.pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots, a.split,       \
+                       a.ctr, a.stack_limit > 0 ? min(a.stack_limit, kProxyStack) : kProxyStack, a.debug_mode,    \
+                       a.redo)
+#define BRE_LAUNCH_PROXY(C, P) BRE_LAUNCH_PROXY_W(C, P, 1)
+        if (counters) {
+            if (a.prefilter) BRE_LAUNCH_PROXY(true, true);
+            else BRE_LAUNCH_PROXY(true, false);
+        } else {
+            if (a.prefilter) BRE_LAUNCH_PROXY(false, true);
+            else BRE_LAUNCH_PROXY(false, false);
+        }
+#undef BRE_LAUNCH_PROXY
+#undef BRE_LAUNCH_PROXY_W
+        hipError_t e3 = hipGetLastError();
+        if (e3 != hipSuccess) return e3;
     }
     const int64_t groups = (a.nseg + kWaveBlock - 1) / kWaveBlock;
     const dim3 grid((unsigned int)(groups * a.split));
+    const uint8_t *redo = kernel == 3 ? a.redo : nullptr;  // kernel 1 as kernel 3's device-side fallback
 #define BRE_LAUNCH_WAVE(C, P)                                                                                   \
     hipLaunchKernelGGL((k_gather_wave<C, P>), grid, dim3(kWaveBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R, \
-                       a.partial, a.seg_counts, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots, a.split,  \
-                       a.ctr, a.debug_mode)
+                       a.partial, a.pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots, a.split,        \
+                       a.ctr, a.debug_mode, redo)
     if (counters) {
         if (a.prefilter) BRE_LAUNCH_WAVE(true, true);
         else BRE_LAUNCH_WAVE(true, false);
@@ -568,7 +941,8 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial,
-                       a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb, a.ctr);
+                       counters ? a.pcnt : nullptr, a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb,
+                       counters ? a.seg_counts : nullptr, a.ctr);
     return hipGetLastError();
 }
 

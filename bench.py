@@ -47,10 +47,11 @@ def parse():
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--radius", type=float, default=0.01)
     ap.add_argument("--kernel", type=int, default=0)
-    ap.add_argument("--leaf-size", type=int, default=4)
-    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet (kernel 1)")
+    ap.add_argument("--leaf-size", type=int, default=1)
+    ap.add_argument("--split", type=int, default=16, help="BVH subtrees per segment packet (kernels 1/3)")
     ap.add_argument("--prefilter", type=int, default=1)
     ap.add_argument("--debug-mode", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
@@ -97,6 +98,8 @@ def main():
                        prefilter=bool(args.prefilter))
     if args.debug_mode:
         g.set_option(100, args.debug_mode)
+    if args.occupancy:
+        g.set_option(102, args.occupancy)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
@@ -174,7 +177,8 @@ def main():
             "segments_per_gpu": nseg,
             "image": [W, H],
             "parallelism": f"image-tiles x{world}, beams replicated",
-            "kernel": "wave-packet" if args.kernel in (0, 1) else "thread-per-segment",
+            "kernel": {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
+                       2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over"}[args.kernel],
             "leaf_size": args.leaf_size,
             "split": args.split,
             "prefilter": bool(args.prefilter),
@@ -189,6 +193,8 @@ def main():
         "beam_evals_per_wave": st["beam_evals"] / max(waves, 1),
         "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / max(waves, 1),
         "useful_beam_evals_per_wave": st["useful_beam_evals"] / max(waves, 1),
+        "max_stack_depth": st["max_stack_depth"],
+        "redo_items": st["redo_items"],
         "prefilter_rejects_per_estimate": st["prefilter_rejects"] / max(nseg, 1),
     }
 

@@ -61,11 +61,13 @@ typedef enum bre_status {
 typedef enum bre_option {
     BRE_OPT_COUNTERS = 1,    /* 0/1: per-segment candidate / contribution / node-visit counting */
     BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
-    BRE_OPT_KERNEL = 3,      /* 0 = auto, 1 = wave-packet traversal, 2 = thread-per-segment */
-    BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 4); applies at next build */
+    BRE_OPT_KERNEL = 3,      /* 0 = auto (3 when leaf size <= 4, else 1), 1 = depth-first wave-packet
+                                traversal, 2 = thread-per-segment, 3 = packet-proxy traversal with
+                                incoherent / overflowing packets handed to kernel 1 on the device */
+    BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
-    BRE_OPT_SPLIT = 6,       /* kernel 1: BVH subtrees per segment packet, power of two 1..64 (default 8) */
-    BRE_OPT_PREFILTER = 7    /* kernel 1: 0/1 conservative line-distance reject before the exact
+    BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 16) */
+    BRE_OPT_PREFILTER = 7    /* kernels 1/3: 0/1 conservative line-distance reject before the exact
                                 closest-point code (default 1; results are identical either way) */
 } bre_option;
 
@@ -84,6 +86,9 @@ typedef struct bre_stats {
     int64_t ccp_wave_evals;  /* kernel 1, counters: exact closest-point executions, per wave */
     int64_t prefilter_rejects; /* kernel 1, counters: lane-level line-distance rejects */
     int64_t useful_beam_evals; /* kernel 1, counters: beam evaluations where >= 1 lane is a candidate */
+    int64_t max_stack_depth;   /* kernel 3, counters: deepest LDS node stack used by any wave */
+    int64_t redo_items;        /* kernel 3, counters: (packet, subtree) items handed to kernel 1
+                                  (incoherent packets or LDS-stack overflow) */
     double build_ms;         /* device time of the last BVH build (timing only) */
     double gather_ms;        /* device time of the last gather kernel (timing only) */
 } bre_stats;

@@ -40,7 +40,7 @@ def test_oracle_reproduces_golden(gold, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 def test_gpu_matches_golden(gold, bre, kernel):
     s = segs_of(gold)
     accum = np.zeros((1024, 3), np.float32)

@@ -36,9 +36,11 @@ def ctxs(bre):
         c.close()
 
 
-@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 @pytest.mark.parametrize("leaf", [1, 4, 8])
 def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
+    if kernel == 3 and leaf > 4:
+        pytest.skip("kernel 3 needs leaf clusters <= 4 (tested in test_kernel3_rejects_large_leaves)")
     beams = synth.fog_beams(3000, seed=12345)
     segs = synth.camera_segments(48, 40, seed=777)
     R = 0.01
@@ -54,7 +56,7 @@ def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     assert st["contributions"] == int(ref["contrib"].sum())
 
 
-@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 def test_bounce_segments_match_oracle(bre, synth, oracle, kernel):
     beams = synth.fog_beams(3000, seed=99)
     segs = synth.bounce_segments(3000, seed=5)
@@ -156,7 +158,7 @@ def test_axis_aligned_rays_and_degenerate_segments(bre, oracle):
     ref = oracle.build(beams).gather(segs, 0.02)
     with bre.BeamGather(0, counters=True) as g:
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        for k in (1, 2):
+        for k in (1, 2, 3):
             g.set_option(bre.OPT_KERNEL, k)
             out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
             assert np.array_equal(out["counts"][:, 0], ref["cand"]), k
@@ -222,12 +224,13 @@ def test_deterministic_per_segment(bre, synth):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("kernel", [1, 3])
 @pytest.mark.parametrize("split", [1, 2, 8, 64])
-def test_subtree_split_matches_oracle(bre, synth, oracle, split):
+def test_subtree_split_matches_oracle(bre, synth, oracle, split, kernel):
     beams = synth.fog_beams(4000, seed=51)
     segs = synth.camera_segments(40, 36, seed=52)
     ref = oracle.build(beams).gather(segs, 0.01)
-    with bre.BeamGather(0, counters=True, kernel=1, split=split) as g:
+    with bre.BeamGather(0, counters=True, kernel=kernel, split=split) as g:
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
         out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=0.01, counts=True)
     assert np.array_equal(out["counts"][:, 0], ref["cand"])
@@ -248,9 +251,38 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         segs = synth.camera_segments(64, 64, seed=64) if kind == "camera" else synth.bounce_segments(4096, seed=65)
         R = 0.01
     outs = []
-    for pf in (False, True):
-        with bre.BeamGather(0, counters=True, kernel=1, prefilter=pf) as g:
+    for k, pf in ((1, False), (1, True), (3, False), (3, True)):
+        with bre.BeamGather(0, counters=True, kernel=k, prefilter=pf) as g:
             g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
             outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True))
     assert np.array_equal(outs[0]["seg_rgb"], outs[1]["seg_rgb"])
     assert np.array_equal(outs[0]["counts"], outs[1]["counts"])
+    # kernel 3 visits beams in a different order: same sets, sums equal to rounding
+    for o in outs[2:]:
+        assert np.array_equal(outs[0]["counts"], o["counts"])
+        assert _seg_close(o["seg_rgb"], outs[0]["seg_rgb"]) <= SEG_RTOL
+    assert np.array_equal(outs[2]["seg_rgb"], outs[3]["seg_rgb"])
+
+
+def test_kernel3_rejects_large_leaves(bre, synth):
+    beams = synth.fog_beams(500)
+    segs = synth.camera_segments(8, 8)
+    with bre.BeamGather(0, kernel=3, leaf_size=8) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        with pytest.raises(bre.BreError):
+            g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)
+
+
+def test_kernel3_stack_overflow_falls_back_exactly(bre, synth, oracle):
+    """Wide incoherent packets over a deep tree can exhaust kernel 3's LDS stack; kernel 1 then
+    recomputes on the device and the results stay exact."""
+    beams = synth.fog_beams(20000, seed=71, mean_length=0.4)
+    segs = synth.camera_segments(48, 32, seed=72)
+    ref = oracle.build(beams).gather(segs, 0.01)
+    with bre.BeamGather(0, counters=True, kernel=3, split=1, leaf_size=1) as g:
+        g.set_option(101, 70)  # internal: 70-entry stack -> most packets overflow
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01, counts=True)
+    assert np.array_equal(out["counts"][:, 0], ref["cand"])
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
