@@ -29,7 +29,7 @@ EXPORTS = [
     "bre_abi_version", "bre_create", "bre_destroy", "bre_last_error", "bre_set_option",
     "bre_set_stream", "bre_synchronize", "bre_get_stats", "bre_set_beams",
     "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
-    "bre_resolve_image",
+    "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell",
 ]
 
 
@@ -48,7 +48,9 @@ class Stats(ctypes.Structure):
                 ("prefilter_rejects", ctypes.c_int64), ("useful_beam_evals", ctypes.c_int64),
                 ("max_stack_depth", ctypes.c_int64), ("redo_items", ctypes.c_int64),
                 ("build_ms", ctypes.c_double),
-                ("gather_ms", ctypes.c_double)]
+                ("gather_ms", ctypes.c_double),
+                ("n_photons", ctypes.c_int64),
+                ("photon_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -100,6 +102,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_beam_radius_at.restype = F
     lib.bre_resolve_image.argtypes = [I64, P, I32, P]
     lib.bre_resolve_image.restype = I32
+    lib.bre_trace_photons.argtypes = [P, P, I64, I32, I32, F, ctypes.POINTER(I64)]
+    lib.bre_trace_photons.restype = I32
+    lib.bre_get_beams.argtypes = [P, I64, P, P, P, P, ctypes.POINTER(I64)]
+    lib.bre_get_beams.restype = I32
+    lib.bre_scene_cornell.argtypes = [P, F, F, F]
+    lib.bre_scene_cornell.restype = None
     _LIB = lib
     return lib
 
@@ -175,6 +183,27 @@ class BeamGather:
             assert t.is_cuda and t.is_contiguous() and str(t.dtype) == "torch.float32"
         self._keep = [start, end, radius, power]
         self._check(self.lib.bre_set_beams_device(self.h, n, _ptr(start), _ptr(end), _ptr(radius), _ptr(power)))
+
+    # ---- photon pass ----
+    def trace_photons(self, scene, n_photons: int, iteration: int = 0, max_depth: int = 5,
+                      radius: float = 0.01) -> int:
+        """Photon pass on the GPU (photonbeam.cpp:362-438): traces, keeps and builds the beams.
+        `scene` is a scene.Scene (ctypes).  Returns the number of beams."""
+        nb = ctypes.c_int64(0)
+        self._check(self.lib.bre_trace_photons(self.h, ctypes.addressof(scene), int(n_photons), int(iteration),
+                                               int(max_depth), float(radius), ctypes.byref(nb)))
+        return nb.value
+
+    def get_beams(self):
+        """Copy the current beam set back: dict start/end (n,3), radius (n,), power (n,3)."""
+        nb = ctypes.c_int64(0)
+        self._check(self.lib.bre_get_beams(self.h, 0, None, None, None, None, ctypes.byref(nb)))
+        n = nb.value
+        out = {"start": np.zeros((n, 3), np.float32), "end": np.zeros((n, 3), np.float32),
+               "radius": np.zeros(n, np.float32), "power": np.zeros((n, 3), np.float32)}
+        self._check(self.lib.bre_get_beams(self.h, n, _ptr(out["start"]), _ptr(out["end"]), _ptr(out["radius"]),
+                                           _ptr(out["power"]), ctypes.byref(nb)))
+        return out
 
     # ---- gather ----
     def gather(self, o, p, d, tmax, pixel=None, R=0.01, npix=0, accum=None, seg_rgb=True, counts=False):

@@ -11,6 +11,7 @@
 
 #include "../../include/bre.h"
 #include "bre_device.h"
+#include "bre_trace.h"
 
 using namespace bre;
 
@@ -68,6 +69,9 @@ struct bre_ctx {
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem counters_buf, roots, partial, pcnt, redo;
+    // photon pass
+    DevMem ph_scene, ph_counts, ph_offsets, ph_tmp;
+    bool beams_kept = false;  // in_* hold the current beam set (bre_get_beams)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bre_stats stats;
 };
@@ -310,7 +314,8 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo};
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo,
+                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp};
     for (DevMem *m : all) m->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -398,10 +403,12 @@ bre_status bre_set_beams(bre_ctx *c, int64_t n, const float *start, const float 
         HIPCHK(c, hipMemcpyAsync(c->in_radius.ptr, radius, N * sizeof(float), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->in_power.ptr, power, N * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     }
+    c->beams_kept = false;
     st = build(c, n, c->in_start.as<float>(), c->in_end.as<float>(), c->in_radius.as<float>(),
                c->in_power.as<float>());
     if (st != BRE_OK) return st;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->beams_kept = true;
     return BRE_OK;
 }
 
@@ -413,7 +420,130 @@ bre_status bre_set_beams_device(bre_ctx *c, int64_t n, const float *start, const
         return fail(c, BRE_ERR_INVALID_ARG, "bre_set_beams_device: null array");
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
+    c->beams_kept = false;
     return build(c, n, start, end, radius, power);
+}
+
+bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photons, int32_t iteration,
+                             int32_t max_depth, float beam_radius, int64_t *n_beams) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (n_beams) *n_beams = 0;
+    if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: null scene");
+    if (n_photons < 0 || iteration < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: negative count");
+    if (max_depth < 1 || max_depth > BRE_MAX_DEPTH)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: max_depth must be in [1, %d]", BRE_MAX_DEPTH);
+    if (scene->n_quads < 1 || scene->n_quads > BRE_MAX_QUADS || scene->light_quad < 0 ||
+        scene->light_quad >= scene->n_quads)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: bad quad count or light index");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    DevScene hs;
+    prepare_scene(scene, 0, 0, &hs);
+    const size_t N = (size_t)n_photons;
+    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
+    HIPCHK(c, c->ph_counts.ensure((N + 1) * sizeof(int32_t)));
+    HIPCHK(c, c->ph_offsets.ensure((N + 1) * sizeof(int64_t)));
+    const size_t tmp = count_scan_temp_bytes(n_photons);
+    HIPCHK(c, c->ph_tmp.ensure(tmp + 16));
+    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    const uint64_t seq0 = (uint64_t)iteration * (uint64_t)n_photons + 1;
+    const DevScene *ds = c->ph_scene.as<DevScene>();
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, launch_photons(ds, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(), nullptr,
+                             nullptr, nullptr, nullptr, nullptr, false, c->stream));
+    HIPCHK(c, launch_count_scan(c->ph_tmp.ptr, c->ph_tmp.cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
+                                n_photons, c->stream));
+    int64_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->ph_offsets.as<int64_t>() + n_photons, sizeof(total), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t B = (size_t)total;
+    if (total > 0) {
+        HIPCHK(c, c->in_start.ensure(B * 3 * sizeof(float)));
+        HIPCHK(c, c->in_end.ensure(B * 3 * sizeof(float)));
+        HIPCHK(c, c->in_radius.ensure(B * sizeof(float)));
+        HIPCHK(c, c->in_power.ensure(B * 3 * sizeof(float)));
+        HIPCHK(c, launch_photons(ds, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
+                                 c->ph_offsets.as<int64_t>(), c->in_start.as<float>(), c->in_end.as<float>(),
+                                 c->in_radius.as<float>(), c->in_power.as<float>(), true, c->stream));
+    }
+    float photon_ms = 0.f;
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&photon_ms, c->ev[0], c->ev[1]));
+    }
+    c->beams_kept = false;
+    st = build(c, total, c->in_start.as<float>(), c->in_end.as<float>(), c->in_radius.as<float>(),
+               c->in_power.as<float>());
+    if (st != BRE_OK) return st;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->beams_kept = true;
+    c->stats.n_photons = n_photons;
+    c->stats.photon_ms = photon_ms;
+    if (n_beams) *n_beams = total;
+    return BRE_OK;
+}
+
+bre_status bre_get_beams(bre_ctx *c, int64_t capacity, float *start, float *end, float *radius, float *power,
+                         int64_t *n_beams) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (capacity < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_get_beams: negative capacity");
+    if (!c->beams_kept && c->nbeams > 0)
+        return fail(c, BRE_ERR_STATE, "bre_get_beams: the beam set came from caller device arrays");
+    if (n_beams) *n_beams = c->nbeams;
+    const int64_t k = capacity < c->nbeams ? capacity : c->nbeams;
+    if (k <= 0) return BRE_OK;
+    if (!start || !end || !radius || !power) return fail(c, BRE_ERR_INVALID_ARG, "bre_get_beams: null array");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    const size_t K = (size_t)k;
+    HIPCHK(c, hipMemcpyAsync(start, c->in_start.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(end, c->in_end.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(radius, c->in_radius.ptr, K * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(power, c->in_power.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
+void bre_scene_cornell(bre_scene *s, float sigma_a, float sigma_s, float g) {
+    if (!s) return;
+    memset(s, 0, sizeof(*s));
+    struct Q {
+        float p0[3], e1[3], e2[3], kd[3];
+    };
+    const float W = 0.73f, R0 = 0.63f, R1 = 0.065f, R2 = 0.05f, G0 = 0.14f, G1 = 0.45f, G2 = 0.091f;
+    const Q qs[7] = {
+        {{0, 0, 0}, {0, 0, 1}, {1, 0, 0}, {W, W, W}},          // floor, normal +y
+        {{0, 1, 0}, {1, 0, 0}, {0, 0, 1}, {W, W, W}},          // ceiling, normal -y
+        {{0, 0, 1}, {0, 1, 0}, {1, 0, 0}, {W, W, W}},          // back wall, normal -z
+        {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {W, W, W}},          // front wall (behind camera), normal +z
+        {{0, 0, 0}, {0, 1, 0}, {0, 0, 1}, {R0, R1, R2}},       // left wall (red), normal +x
+        {{1, 0, 0}, {0, 0, 1}, {0, 1, 0}, {G0, G1, G2}},       // right wall (green), normal -x
+        {{0.35f, 0.999f, 0.35f}, {0.3f, 0, 0}, {0, 0, 0.3f}, {0, 0, 0}},  // light, normal -y
+    };
+    s->n_quads = 7;
+    for (int i = 0; i < 7; ++i) {
+        memcpy(s->quads[i].p0, qs[i].p0, 12);
+        memcpy(s->quads[i].e1, qs[i].e1, 12);
+        memcpy(s->quads[i].e2, qs[i].e2, 12);
+        memcpy(s->quads[i].kd, qs[i].kd, 12);
+    }
+    s->light_quad = 6;
+    s->light_L[0] = 17.f;
+    s->light_L[1] = 12.f;
+    s->light_L[2] = 4.f;
+    s->has_medium = 1;
+    for (int k = 0; k < 3; ++k) {
+        s->sigma_a[k] = sigma_a;
+        s->sigma_s[k] = sigma_s;
+    }
+    s->g = g;
+    const float pos[3] = {0.5f, 0.5f, 0.02f}, look[3] = {0.5f, 0.5f, 1.f}, up[3] = {0, 1, 0};
+    memcpy(s->cam_pos, pos, 12);
+    memcpy(s->cam_look, look, 12);
+    memcpy(s->cam_up, up, 12);
+    s->cam_fov_deg = 60.f;
 }
 
 bre_status bre_gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d,

@@ -1,0 +1,220 @@
+// bre_trace.h — scene evaluation for the on-device photon and camera passes (host + device).
+//
+// Float arithmetic follows the reference's operation order (see the file:line next to each
+// function) and is compiled without FMA contraction, with correctly rounded division and sqrt,
+// and with the transcendentals of include/bre_fmath.h, so a photon path on the GPU takes the
+// same random decisions and produces the same beam bits as the CPU restatement in oracle/.
+#pragma once
+
+#include "../../include/bre_fmath.h"
+#include "../../include/bre_scene.h"
+#include "bre_math.h"
+
+namespace bre {
+
+#define BRE_TD __host__ __device__ __forceinline__
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kInvPi = 0.31830988618379067154f;
+constexpr float kInv4Pi = 0.07957747154594766788f;
+constexpr float kPiOver2 = 1.57079632679489661923f;
+constexpr float kPiOver4 = 0.78539816339744830961f;
+constexpr float kOneMinusEps = 0x1.fffffep-1f;
+constexpr float kMaxFloat = 3.402823466e+38f;
+
+// gamma(n) of pbrt.h:263-265 in float
+BRE_TD float gamma_n(int n) {
+    const float eps = 0x1p-24f;
+    return (n * eps) / (1 - n * eps);
+}
+
+// ---- PCG32 as pbrt seeds and uses it (rng.h:78-85, 129-144) ----
+struct Pcg {
+    uint64_t state, inc;
+};
+BRE_TD uint32_t pcg_next(Pcg &r) {
+    const uint64_t old = r.state;
+    r.state = old * 0x5851f42d4c957f2dULL + r.inc;
+    const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+}
+BRE_TD void pcg_seed(Pcg &r, uint64_t seq) {
+    r.state = 0u;
+    r.inc = (seq << 1u) | 1u;
+    (void)pcg_next(r);
+    r.state += 0x853c49e6748fea9bULL;
+    (void)pcg_next(r);
+}
+BRE_TD float pcg_float(Pcg &r) {
+    return smin(kOneMinusEps, (float)pcg_next(r) * 0x1p-32f);  // std::min(OneMinusEpsilon, .)
+}
+// Get2D of the reference's samplers: Point2f(Get1D(), Get1D()) built by g++ right to left
+// (photonbeam.cpp:207-212, 239-241), so x is the second draw.
+BRE_TD void pcg_2d(Pcg &r, float &x, float &y) {
+    const float first = pcg_float(r);
+    const float second = pcg_float(r);
+    x = second;
+    y = first;
+}
+
+// ---- vector helpers (geometry.h) ----
+BRE_TD f3 neg3(f3 a) { return mk(-a.x, -a.y, -a.z); }
+BRE_TD f3 abs3(f3 a) { return mk(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+BRE_TD f3 normalize3(f3 v) { return div3(v, len3(v)); }
+BRE_TD f3 ray_at(f3 o, f3 d, float t) { return add3(o, scale3(d, t)); }
+// CoordinateSystem, geometry.h:1020-1027
+BRE_TD void coord_system(f3 v1, f3 &v2, f3 &v3) {
+    if (fabsf(v1.x) > fabsf(v1.y))
+        v2 = div3(mk(-v1.z, 0, v1.x), sqrtf(v1.x * v1.x + v1.z * v1.z));
+    else
+        v2 = div3(mk(0, v1.z, -v1.y), sqrtf(v1.y * v1.y + v1.z * v1.z));
+    v3 = cross3d(v1, v2);
+}
+BRE_TD float next_up(float v) {
+    if (v == __builtin_huge_valf()) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = bre_f2u(v);
+    if (v >= 0) ++ui;
+    else --ui;
+    return bre_u2f(ui);
+}
+BRE_TD float next_down(float v) {
+    if (v == -__builtin_huge_valf()) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = bre_f2u(v);
+    if (v > 0) --ui;
+    else ++ui;
+    return bre_u2f(ui);
+}
+// OffsetRayOrigin, geometry.h:1438-1458
+BRE_TD f3 offset_origin(f3 p, f3 perr, f3 n, f3 w) {
+    const float d = dot3(abs3(n), perr);
+    f3 off = scale3(n, d);
+    if (dot3(w, n) < 0) off = neg3(off);
+    f3 po = add3(p, off);
+    po.x = off.x > 0 ? next_up(po.x) : (off.x < 0 ? next_down(po.x) : po.x);
+    po.y = off.y > 0 ? next_up(po.y) : (off.y < 0 ? next_down(po.y) : po.y);
+    po.z = off.z > 0 ? next_up(po.z) : (off.z < 0 ? next_down(po.z) : po.z);
+    return po;
+}
+
+// ---- sampling (sampling.cpp:113-133, sampling.h:159-165) ----
+BRE_TD f3 cosine_hemisphere(float ux, float uy) {
+    const float ox = 2.f * ux - 1, oy = 2.f * uy - 1;
+    float dx = 0, dy = 0;
+    if (!(ox == 0 && oy == 0)) {
+        float theta, r;
+        if (fabsf(ox) > fabsf(oy)) {
+            r = ox;
+            theta = kPiOver4 * (oy / ox);
+        } else {
+            r = oy;
+            theta = kPiOver2 - kPiOver4 * (ox / oy);
+        }
+        float s, c;
+        bre_sincosf(theta, &s, &c);
+        dx = c * r;
+        dy = s * r;
+    }
+    return mk(dx, dy, sqrtf(smax(0.f, 1 - dx * dx - dy * dy)));
+}
+
+// ---- Henyey-Greenstein Sample_p (medium.cpp:194-213); the returned pdf is unused here ----
+BRE_TD f3 hg_sample(float g, f3 wo, float u0, float u1) {
+    float cos_t;
+    if ((double)fabsf(g) < 1e-3) {  // std::abs(g) < 1e-3 compares in double
+        cos_t = 1 - 2 * u0;
+    } else {
+        const float sq = (1 - g * g) / (1 - g + 2 * g * u0);
+        cos_t = (1 + g * g - sq * sq) / (2 * g);
+    }
+    const float sin_t = sqrtf(smax(0.f, 1 - cos_t * cos_t));
+    const float phi = 2 * kPi * u1;
+    f3 v1, v2;
+    coord_system(wo, v1, v2);
+    float sp, cp;
+    bre_sincosf(phi, &sp, &cp);
+    // SphericalDirection(sinT, cosT, phi, v1, v2, -wo), geometry.h:1465-1470
+    return add3(add3(scale3(v1, sin_t * cp), scale3(v2, sin_t * sp)), scale3(neg3(wo), cos_t));
+}
+
+// ---- scene on the device ----
+struct PQuad {
+    f3 p0, e1, e2, n, ss, ts;
+    float kd[3];
+    float inv_e1sq, inv_e2sq, area;
+    int absorb;  // kd all zero: no BxDF
+    int pad;
+};
+
+struct DevScene {
+    int n_quads, light, medium, pad;
+    float Le[3];
+    float sigma_t[3];
+    float g;
+    // pinhole camera (perspective.cpp with lensradius 0): world-space frame and raster mapping
+    f3 cam_o, cam_x, cam_y, cam_z;
+    float cam_sx, cam_sy;  // screen window half-extents (tan(fov/2) * aspect terms)
+    PQuad q[BRE_MAX_QUADS];
+};
+
+// host: derive per-quad constants exactly as oracle/bre_oracle_photon.cpp make_scene does
+void prepare_scene(const bre_scene *s, int width, int height, DevScene *out);
+
+struct Hit {
+    f3 p, perr;
+    int quad;
+};
+
+// closest hit over all quads; strict <, lowest index wins a tie; t in (0, tmax)
+__device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, float &tmax, Hit &h) {
+    bool hit = false;
+    for (int i = 0; i < S.n_quads; ++i) {
+        const PQuad &q = S.q[i];
+        const float denom = dot3(q.n, d);
+        if (denom == 0) continue;
+        const float t = dot3(q.n, sub3(q.p0, o)) / denom;
+        if (!(t > 0 && t < tmax)) continue;
+        const f3 rel = sub3(ray_at(o, d, t), q.p0);
+        const float u = dot3(rel, q.e1) * q.inv_e1sq;
+        const float v = dot3(rel, q.e2) * q.inv_e2sq;
+        if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) continue;
+        tmax = t;
+        const f3 ue1 = scale3(q.e1, u), ve2 = scale3(q.e2, v);
+        h.p = add3(add3(q.p0, ue1), ve2);
+        h.perr = scale3(add3(add3(abs3(q.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
+        h.quad = i;
+        hit = true;
+    }
+    return hit;
+}
+
+// HomogeneousMedium::Tr, homogeneous.cpp:44-48
+__device__ __forceinline__ void medium_tr(const DevScene &S, f3 d, float tmax, float tr[3]) {
+    const float x = smin(tmax * len3(d), kMaxFloat);
+    for (int c = 0; c < 3; ++c) tr[c] = bre_expf(-S.sigma_t[c] * x);
+}
+
+// HomogeneousMedium::Sample distance part, homogeneous.cpp:50-60 (two draws)
+__device__ __forceinline__ bool medium_sample(const DevScene &S, Pcg &rng, f3 d, float tmax, float &t) {
+    int ch = (int)(pcg_float(rng) * 3);
+    ch = (2 < ch) ? 2 : ch;  // std::min(ch, 2)
+    const float st = ch == 0 ? S.sigma_t[0] : (ch == 1 ? S.sigma_t[1] : S.sigma_t[2]);
+    const float dist = -bre_logf(1 - pcg_float(rng)) / st;
+    t = smin(dist * len3(d), tmax);
+    return t < tmax;
+}
+
+BRE_TD bool black3(const float v[3]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
+BRE_TD float lum3(const float v[3]) { return 0.212671f * v[0] + 0.715160f * v[1] + 0.072169f * v[2]; }
+
+// photon pass launchers (bre_photon.hip)
+hipError_t launch_photons(const DevScene *scene, int64_t n, uint64_t seq0, int max_depth, float radius,
+                          int32_t *counts, const int64_t *offsets, float *start, float *end, float *rad,
+                          float *power, bool emit, hipStream_t s);
+size_t count_scan_temp_bytes(int64_t n);
+hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n,
+                             hipStream_t s);
+
+}  // namespace bre

@@ -1,0 +1,77 @@
+"""ctypes mirror of include/bre_scene.h and the benchmark scene of SURVEY.md §8d (C1/C2).
+
+Pure data: the same struct the C ABI takes (``bre_trace_photons``) and the oracle restatement
+reads (``ora_trace_photons``).  ``cornell_scene`` must stay identical to libbre's
+``bre_scene_cornell`` (checked byte for byte by tests/test_photon_oracle.py).
+"""
+from __future__ import annotations
+
+import ctypes
+
+MAX_QUADS = 64
+MAX_DEPTH = 16
+
+F3 = ctypes.c_float * 3
+
+
+class Quad(ctypes.Structure):
+    _fields_ = [("p0", F3), ("e1", F3), ("e2", F3), ("kd", F3)]
+
+
+class Scene(ctypes.Structure):
+    _fields_ = [("n_quads", ctypes.c_int32), ("light_quad", ctypes.c_int32), ("light_L", F3),
+                ("has_medium", ctypes.c_int32), ("sigma_a", F3), ("sigma_s", F3), ("g", ctypes.c_float),
+                ("cam_pos", F3), ("cam_look", F3), ("cam_up", F3), ("cam_fov_deg", ctypes.c_float),
+                ("quads", Quad * MAX_QUADS)]
+
+    def to_bytes(self) -> bytes:
+        return ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self))
+
+
+def _f3(v):
+    return F3(*[float(x) for x in v])
+
+
+def make_scene(quads, light_quad, light_L, sigma_a=None, sigma_s=None, g=0.0,
+               cam_pos=(0.5, 0.5, 0.02), cam_look=(0.5, 0.5, 1.0), cam_up=(0.0, 1.0, 0.0), fov=60.0) -> Scene:
+    """quads: list of (p0, e1, e2, kd); medium present iff sigma_a is given (RGB or scalar)."""
+    s = Scene()
+    ctypes.memset(ctypes.addressof(s), 0, ctypes.sizeof(s))
+    assert 1 <= len(quads) <= MAX_QUADS
+    s.n_quads = len(quads)
+    for i, (p0, e1, e2, kd) in enumerate(quads):
+        s.quads[i].p0, s.quads[i].e1, s.quads[i].e2, s.quads[i].kd = _f3(p0), _f3(e1), _f3(e2), _f3(kd)
+    s.light_quad = light_quad
+    s.light_L = _f3(light_L)
+    if sigma_a is not None:
+        rgb = (lambda v: (v, v, v) if isinstance(v, (int, float)) else tuple(v))
+        s.has_medium = 1
+        s.sigma_a = _f3(rgb(sigma_a))
+        s.sigma_s = _f3(rgb(sigma_s))
+        s.g = float(g)
+    s.cam_pos, s.cam_look, s.cam_up = _f3(cam_pos), _f3(cam_look), _f3(cam_up)
+    s.cam_fov_deg = float(fov)
+    return s
+
+
+WHITE = (0.73, 0.73, 0.73)
+RED = (0.63, 0.065, 0.05)
+GREEN = (0.14, 0.45, 0.091)
+
+
+def cornell_quads():
+    """Unit-cube Cornell box, normals inward (normal = normalize(e1 x e2)); light last."""
+    return [
+        ((0, 0, 0), (0, 0, 1), (1, 0, 0), WHITE),     # floor
+        ((0, 1, 0), (1, 0, 0), (0, 0, 1), WHITE),     # ceiling
+        ((0, 0, 1), (0, 1, 0), (1, 0, 0), WHITE),     # back wall
+        ((0, 0, 0), (1, 0, 0), (0, 1, 0), WHITE),     # front wall (behind the camera)
+        ((0, 0, 0), (0, 1, 0), (0, 0, 1), RED),       # left wall
+        ((1, 0, 0), (0, 0, 1), (0, 1, 0), GREEN),     # right wall
+        ((0.35, 0.999, 0.35), (0.3, 0, 0), (0, 0, 0.3), (0, 0, 0)),  # area light, facing down
+    ]
+
+
+def cornell_scene(sigma_a: float = 0.05, sigma_s: float = 0.5, g: float = 0.0) -> Scene:
+    """Cornell box in homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)."""
+    return make_scene(cornell_quads(), 6, (17.0, 12.0, 4.0), sigma_a, sigma_s, g)

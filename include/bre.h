@@ -40,6 +40,8 @@
 
 #include <stdint.h>
 
+#include "bre_scene.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -91,6 +93,8 @@ typedef struct bre_stats {
                                   (incoherent packets or LDS-stack overflow) */
     double build_ms;         /* device time of the last BVH build (timing only) */
     double gather_ms;        /* device time of the last gather kernel (timing only) */
+    int64_t n_photons;       /* photons traced by the last bre_trace_photons */
+    double photon_ms;        /* device time of the last photon pass, both passes (timing only) */
 } bre_stats;
 
 /* ---- context ---- */
@@ -134,6 +138,21 @@ bre_status bre_gather_device(bre_ctx *ctx, int64_t nseg, const float *d_seg_o_xy
                              const float *d_seg_tmax, const int32_t *d_seg_pixel,
                              float beam_radius_cur, int64_t npix, float *d_accum_rgb,
                              float *d_seg_rgb, int32_t *d_seg_counts);
+
+/* ---- photon pass (replaces photonbeam.cpp:362-437: emission, TracePhotonBeamRecursive and the
+   merge into one beam vector, then the PhotonBeamBVH build of :438) ----
+   Traces photons [0, n_photons) of `iteration` on the device (photon i uses PCG32 sequence
+   iteration*n_photons + i + 1, :386-389), keeps the beams on the device in the reference's order
+   (photon-major, push order within a photon) and builds the BVH over them, exactly as
+   bre_set_beams would with the same arrays.  max_depth in [1, BRE_MAX_DEPTH]; beam_radius is the
+   iteration's currentBeamRadius.  *n_beams (may be NULL) receives the beam count.  Synchronous. */
+bre_status bre_trace_photons(bre_ctx *ctx, const bre_scene *scene, int64_t n_photons, int32_t iteration,
+                             int32_t max_depth, float beam_radius, int64_t *n_beams);
+/* Copy the current beam set (from bre_set_beams or bre_trace_photons) back to host arrays in
+   their original order; at most `capacity` beams are written, *n_beams receives the set size.
+   BRE_ERR_STATE after bre_set_beams_device (the library keeps no copy of caller device arrays). */
+bre_status bre_get_beams(bre_ctx *ctx, int64_t capacity, float *start_xyz, float *end_xyz, float *radius,
+                         float *power_end_rgb, int64_t *n_beams);
 
 /* ---- integrator helpers (photonbeam.cpp:354-356, 562, 578) ---- */
 /* R_i for iteration i: R_{k+1} = R_k * (k + alpha) / (k + 1), R_0 = initial, in float. */

@@ -40,6 +40,16 @@ class Oracle:
         lib.ora_bvh_free.argtypes = [P]
         lib.ora_gather.argtypes = [P, I64, P, P, P, P, P, F, P, P, P, P, P, I32, I64]
         lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P]
+        U64 = ctypes.c_uint64
+        lib.ora_trace_photons.argtypes = [P, I64, I32, I32, F, I64, P, P, P, P, P]
+        lib.ora_trace_photons.restype = I64
+        lib.ora_pcg32.argtypes = [U64, I64, I32, P]
+        lib.ora_pcg32_srandom.argtypes = [U64, U64, I64, P]
+        lib.ora_hg_sample.argtypes = [F, I64, P, P, P, P]
+        lib.ora_hg_p.argtypes = [F, I64, P, P, P]
+        lib.ora_homogeneous_tr.argtypes = [P, P, I64, P, P, P]
+        lib.ora_cosine_hemisphere.argtypes = [I64, P, P]
+        lib.ora_fmath.argtypes = [I32, I64, P, P]
 
     # -- primitives --
     def slab_pad(self) -> float:
@@ -65,6 +75,63 @@ class Oracle:
 
     def radius_at(self, r0, alpha, it):
         return float(self.lib.ora_radius_at(r0, alpha, it))
+
+    # -- photon pass (oracle/bre_oracle_photon.cpp) --
+    def trace_photons(self, scene, n_photons, iteration=0, max_depth=5, radius=0.01):
+        """Recursive restatement of the photon pass: beams in the reference's order + per-photon counts."""
+        sp = ctypes.addressof(scene)
+        counts = np.zeros(n_photons, np.int32)
+        n = int(self.lib.ora_trace_photons(sp, n_photons, iteration, max_depth, float(radius), 0,
+                                           None, None, None, None, _p(counts)))
+        out = {"start": np.zeros((n, 3), np.float32), "end": np.zeros((n, 3), np.float32),
+               "radius": np.zeros(n, np.float32), "power": np.zeros((n, 3), np.float32)}
+        n2 = self.lib.ora_trace_photons(sp, n_photons, iteration, max_depth, float(radius), n, _p(out["start"]),
+                                        _p(out["end"]), _p(out["radius"]), _p(out["power"]), None)
+        assert n2 == n
+        out["counts"] = counts
+        return out
+
+    def pcg32(self, seq, n, as_float=False):
+        out = np.zeros(n, np.uint32)
+        self.lib.ora_pcg32(seq, n, int(as_float), _p(out))
+        return out.view(np.float32) if as_float else out
+
+    def pcg32_srandom(self, initstate, initseq, n):
+        out = np.zeros(n, np.uint32)
+        self.lib.ora_pcg32_srandom(initstate, initseq, n, _p(out))
+        return out
+
+    def hg_sample(self, g, wo, u):
+        wo, u = (np.ascontiguousarray(x, np.float32) for x in (wo, u))
+        n = wo.shape[0]
+        wi = np.zeros((n, 3), np.float32)
+        pdf = np.zeros(n, np.float32)
+        self.lib.ora_hg_sample(float(g), n, _p(wo), _p(u), _p(wi), _p(pdf))
+        return wi, pdf
+
+    def hg_p(self, g, wo, wi):
+        wo, wi = (np.ascontiguousarray(x, np.float32) for x in (wo, wi))
+        p = np.zeros(wo.shape[0], np.float32)
+        self.lib.ora_hg_p(float(g), wo.shape[0], _p(wo), _p(wi), _p(p))
+        return p
+
+    def homogeneous_tr(self, sigma_a, sigma_s, d, tmax):
+        sa, ss, d, tmax = (np.ascontiguousarray(x, np.float32) for x in (sigma_a, sigma_s, d, tmax))
+        tr = np.zeros((d.shape[0], 3), np.float32)
+        self.lib.ora_homogeneous_tr(_p(sa), _p(ss), d.shape[0], _p(d), _p(tmax), _p(tr))
+        return tr
+
+    def cosine_hemisphere(self, u):
+        u = np.ascontiguousarray(u, np.float32)
+        w = np.zeros((u.shape[0], 3), np.float32)
+        self.lib.ora_cosine_hemisphere(u.shape[0], _p(u), _p(w))
+        return w
+
+    def fmath(self, kind, x):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        self.lib.ora_fmath({"log": 0, "exp": 1, "sin": 2, "cos": 3}[kind], x.shape[0], _p(x), _p(y))
+        return y
 
     # -- gather through the reference SAH tree --
     def build(self, beams, sqrt_mode=0):
@@ -133,8 +200,9 @@ _ORACLE = None
 def load_oracle() -> Oracle:
     global _ORACLE
     if _ORACLE is None:
-        src = os.path.join(ORACLE_DIR, "bre_oracle.cpp")
-        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("bre_oracle.cpp", "bre_oracle_photon.cpp")]
+        srcs += [os.path.join(ROOT, "include", f) for f in ("bre_fmath.h", "bre_scene.h")]
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
             subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
         _ORACLE = Oracle(ctypes.CDLL(ORACLE_SO))
     return _ORACLE

@@ -1,0 +1,433 @@
+"""Independent pure-Python restatement of the photon pass (test infrastructure).
+
+Written from the reference text (src/integrators/photonbeam.cpp:258-325, 383-421 and the pbrt
+functions they call), NOT from oracle/bre_oracle_photon.cpp, with every float operation done on
+numpy float32 scalars (IEEE single, like the reference's `Float`) and `Cross` in Python floats
+(double, geometry.h:957-963).  The transcendentals restate include/bre_fmath.h (Cephes) in the
+same float32 arithmetic.  Slow (pure Python): used on a few hundred photons to pin the C++ oracle.
+"""
+from __future__ import annotations
+
+import math
+import struct
+
+import numpy as np
+
+f32 = np.float32
+ONE_MINUS_EPS = f32(struct.unpack("<f", struct.pack("<I", 0x3F7FFFFF))[0])
+INF = f32(np.inf)
+MAXF = f32(3.402823466e38)
+PI = f32(3.14159265358979323846)
+INV_PI = f32(0.31830988618379067154)
+PI_OVER_2 = f32(1.57079632679489661923)
+PI_OVER_4 = f32(0.78539816339744830961)
+MASK64 = (1 << 64) - 1
+
+
+def _bits(x):
+    return int(np.array(x, np.float32).view(np.uint32))
+
+
+def _from_bits(u):
+    return np.array(u & 0xFFFFFFFF, np.uint32).view(np.float32)[()]
+
+
+# ---- include/bre_fmath.h restated ----
+def _roundf(x):
+    big = f32(8388608.0)
+    a = -x if x < 0 else x
+    if not (a < big):
+        return x
+    r = f32(a + f32(0.5))
+    t = f32(f32(r + big) - big)
+    if t > r:
+        t = f32(t - f32(1))
+    return -t if x < 0 else t
+
+
+def _pow2i(n):
+    return _from_bits((n + 127) << 23)
+
+
+def logf(x):
+    x = f32(x)
+    u = _bits(x)
+    e = (u >> 23) & 0xFF
+    if e == 0:
+        x = f32(x * f32(16777216.0))
+        u = _bits(x)
+        e = ((u >> 23) & 0xFF) - 24
+    e -= 126
+    m = _from_bits((u & 0x807FFFFF) | 0x3F000000)
+    if m < f32(0.70710678118654752440):
+        e -= 1
+        m = f32(f32(m + m) - f32(1))
+    else:
+        m = f32(m - f32(1))
+    z = f32(m * m)
+    y = f32(7.0376836292e-2)
+    for c in (-1.1514610310e-1, 1.1676998740e-1, -1.2420140846e-1, 1.4249322787e-1, -1.6668057665e-1,
+              2.0000714765e-1, -2.4999993993e-1, 3.3333331174e-1):
+        y = f32(f32(y * m) + f32(c))
+    y = f32(f32(y * m) * z)
+    fe = f32(e)
+    y = f32(y + f32(f32(-2.12194440e-4) * fe))
+    y = f32(y + f32(f32(-0.5) * z))
+    r = f32(m + y)
+    return f32(r + f32(f32(0.693359375) * fe))
+
+
+def expf(x):
+    x = f32(x)
+    if x > f32(88.72283935546875):
+        return INF
+    if x < f32(-103.972084045410):
+        return f32(0)
+    n = _roundf(f32(x * f32(1.44269504088896341)))
+    r = f32(x - f32(n * f32(0.693359375)))
+    r = f32(r - f32(n * f32(-2.12194440e-4)))
+    z = f32(r * r)
+    p = f32(1.9875691500e-4)
+    for c in (1.3981999507e-3, 8.3334519073e-3, 4.1665795894e-2, 1.6666665459e-1, 5.0000001201e-1):
+        p = f32(f32(p * r) + f32(c))
+    p = f32(f32(f32(p * z) + r) + f32(1))
+    ni = int(n)
+    if ni < -126:
+        p = f32(p * _pow2i(-126))
+        ni += 126
+        if ni < -126:
+            return f32(0)
+    if ni > 127:
+        p = f32(p * _pow2i(127))
+        ni -= 127
+    return f32(p * _pow2i(ni))
+
+
+def sincosf(x):
+    x = f32(x)
+    sign_s = f32(1)
+    if x < 0:
+        x = -x
+        sign_s = f32(-1)
+    j = int(f32(x * f32(1.27323954473516)))
+    if j & 1:
+        j += 1
+    y = f32(j)
+    j &= 7
+    z = f32(f32(f32(x - f32(y * f32(0.78515625))) - f32(y * f32(2.4187564849853515625e-4)))
+            - f32(y * f32(3.77489497744594108e-8)))
+    sign_c = f32(1)
+    if j > 3:
+        j -= 4
+        sign_s = -sign_s
+        sign_c = -sign_c
+    if j > 1:
+        sign_c = -sign_c
+    zz = f32(z * z)
+    ps = f32(-1.9515295891e-4)
+    ps = f32(f32(ps * zz) + f32(8.3321608736e-3))
+    ps = f32(f32(ps * zz) + f32(-1.6666654611e-1))
+    ps = f32(f32(f32(ps * zz) * z) + z)
+    pc = f32(2.443315711809948e-5)
+    pc = f32(f32(pc * zz) + f32(-1.388731625493765e-3))
+    pc = f32(f32(pc * zz) + f32(4.166664568298827e-2))
+    pc = f32(f32(pc * zz) * zz)
+    pc = f32(f32(pc - f32(f32(0.5) * zz)) + f32(1))
+    if j in (1, 2):
+        return f32(sign_s * pc), f32(sign_c * ps)
+    return f32(sign_s * ps), f32(sign_c * pc)
+
+
+# ---- PCG32 (rng.h) ----
+class RNG:
+    def __init__(self, seq):
+        self.state = 0
+        self.inc = ((seq << 1) | 1) & MASK64
+        self.u32()
+        self.state = (self.state + 0x853C49E6748FEA9B) & MASK64
+        self.u32()
+
+    def u32(self):
+        old = self.state
+        self.state = (old * 0x5851F42D4C957F2D + self.inc) & MASK64
+        xs = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
+        rot = old >> 59
+        return ((xs >> rot) | (xs << ((-rot) & 31))) & 0xFFFFFFFF
+
+    def uniform(self):
+        v = f32(f32(self.u32()) * f32(2.0 ** -32))
+        return v if v < ONE_MINUS_EPS else ONE_MINUS_EPS
+
+    def get2d(self):
+        first = self.uniform()
+        second = self.uniform()
+        return second, first  # g++: Point2f(Get1D(), Get1D()) evaluated right to left
+
+
+# ---- vectors: tuples of float32 ----
+def add(a, b):
+    return tuple(f32(x + y) for x, y in zip(a, b))
+
+
+def sub(a, b):
+    return tuple(f32(x - y) for x, y in zip(a, b))
+
+
+def mul(a, s):
+    return tuple(f32(s * x) for x in a)
+
+
+def div(a, s):
+    inv = f32(f32(1) / s)
+    return tuple(f32(x * inv) for x in a)
+
+
+def dot(a, b):
+    return f32(f32(f32(a[0] * b[0]) + f32(a[1] * b[1])) + f32(a[2] * b[2]))
+
+
+def length(a):
+    return f32(np.sqrt(dot(a, a)))
+
+
+def normalize(a):
+    return div(a, length(a))
+
+
+def cross(a, b):
+    ax, ay, az = (float(x) for x in a)
+    bx, by, bz = (float(x) for x in b)
+    return (f32(ay * bz - az * by), f32(az * bx - ax * bz), f32(ax * by - ay * bx))
+
+
+def vabs(a):
+    return tuple(f32(abs(x)) for x in a)
+
+
+def coordinate_system(v1):
+    if abs(v1[0]) > abs(v1[1]):
+        v2 = div((-v1[2], f32(0), v1[0]), f32(np.sqrt(f32(f32(v1[0] * v1[0]) + f32(v1[2] * v1[2])))))
+    else:
+        v2 = div((f32(0), v1[2], -v1[1]), f32(np.sqrt(f32(f32(v1[1] * v1[1]) + f32(v1[2] * v1[2])))))
+    return v2, cross(v1, v2)
+
+
+def next_up(v):
+    if v == INF:
+        return v
+    if v == 0:
+        v = f32(0)
+    u = _bits(v)
+    return _from_bits(u + 1 if v >= 0 else u - 1)
+
+
+def next_down(v):
+    if v == -INF:
+        return v
+    if v == 0:
+        v = f32(-0.0)
+    u = _bits(v)
+    return _from_bits(u - 1 if v > 0 else u + 1)
+
+
+def offset_origin(p, perr, n, w):
+    d = dot(vabs(n), perr)
+    off = mul(n, d)
+    if dot(w, n) < 0:
+        off = tuple(-x for x in off)
+    po = list(add(p, off))
+    for i in range(3):
+        if off[i] > 0:
+            po[i] = next_up(po[i])
+        elif off[i] < 0:
+            po[i] = next_down(po[i])
+    return tuple(po)
+
+
+def gamma(n):
+    e = f32(2.0 ** -24)
+    return f32(f32(n * e) / f32(f32(1) - f32(n * e)))
+
+
+def cosine_hemisphere(ux, uy):
+    ox, oy = f32(f32(2 * ux) - f32(1)), f32(f32(2 * uy) - f32(1))
+    if ox == 0 and oy == 0:
+        dx = dy = f32(0)
+    else:
+        if abs(ox) > abs(oy):
+            r, theta = ox, f32(PI_OVER_4 * f32(oy / ox))
+        else:
+            r, theta = oy, f32(PI_OVER_2 - f32(PI_OVER_4 * f32(ox / oy)))
+        s, c = sincosf(theta)
+        dx, dy = f32(c * r), f32(s * r)
+    t = f32(f32(f32(1) - f32(dx * dx)) - f32(dy * dy))
+    return (dx, dy, f32(np.sqrt(t if t > 0 else f32(0))))
+
+
+def hg_sample(g, wo, u0, u1):
+    g = f32(g)
+    if abs(float(g)) < 1e-3:
+        cos_t = f32(f32(1) - f32(2 * u0))
+    else:
+        sq = f32(f32(f32(1) - f32(g * g)) / f32(f32(f32(1) - g) + f32(f32(2 * g) * u0)))
+        cos_t = f32(f32(f32(f32(1) + f32(g * g)) - f32(sq * sq)) / f32(2 * g))
+    m = f32(f32(1) - f32(cos_t * cos_t))
+    sin_t = f32(np.sqrt(m if m > 0 else f32(0)))
+    phi = f32(f32(2 * PI) * u1)
+    v1, v2 = coordinate_system(wo)
+    sp, cp = sincosf(phi)
+    return add(add(mul(v1, f32(sin_t * cp)), mul(v2, f32(sin_t * sp))), mul(tuple(-x for x in wo), cos_t))
+
+
+class Scene:
+    def __init__(self, s):
+        self.quads = []
+        for i in range(s.n_quads):
+            q = s.quads[i]
+            p0, e1, e2 = (tuple(f32(x) for x in v) for v in (q.p0, q.e1, q.e2))
+            c = cross(e1, e2)
+            n = normalize(c)
+            ss = normalize(e1)
+            self.quads.append(dict(p0=p0, e1=e1, e2=e2, n=n, ss=ss, ts=cross(n, ss), area=length(c),
+                                   ie1=f32(f32(1) / dot(e1, e1)), ie2=f32(f32(1) / dot(e2, e2)),
+                                   kd=tuple(f32(x) for x in q.kd)))
+        self.light = s.light_quad
+        self.Le = tuple(f32(x) for x in s.light_L)
+        self.medium = bool(s.has_medium)
+        self.sigma_t = tuple(f32(f32(a) + f32(b)) for a, b in zip(s.sigma_a, s.sigma_s))
+        self.g = f32(s.g)
+
+    def intersect(self, o, d):
+        best = None
+        tmax = INF
+        for i, q in enumerate(self.quads):
+            den = dot(q["n"], d)
+            if den == 0:
+                continue
+            t = f32(dot(q["n"], sub(q["p0"], o)) / den)
+            if not (t > 0 and t < tmax):
+                continue
+            rel = sub(add(o, mul(d, t)), q["p0"])
+            u = f32(dot(rel, q["e1"]) * q["ie1"])
+            v = f32(dot(rel, q["e2"]) * q["ie2"])
+            if not (0 <= u <= 1 and 0 <= v <= 1):
+                continue
+            tmax = t
+            ue1, ve2 = mul(q["e1"], u), mul(q["e2"], v)
+            p = add(add(q["p0"], ue1), ve2)
+            perr = mul(add(add(vabs(q["p0"]), vabs(ue1)), vabs(ve2)), gamma(6))
+            best = (p, perr, i)
+        return best, tmax
+
+    def tr(self, d, tmax):
+        x = f32(tmax * length(d))
+        x = MAXF if MAXF < x else x
+        return tuple(expf(f32(f32(-st) * x)) for st in self.sigma_t)
+
+
+def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
+    """Beams of one photon, in the reference's push order: list of (start, end, radius, power)."""
+    rng = RNG(seq)
+    out = []
+    rng.uniform()  # light choice (one light)
+    u0 = rng.get2d()
+    u1 = rng.get2d()
+    rng.uniform()  # time
+    L = sc.quads[sc.light]
+    ue1, ve2 = mul(L["e1"], u0[0]), mul(L["e2"], u0[1])
+    p = add(add(L["p0"], ue1), ve2)
+    perr = mul(add(add(vabs(L["p0"]), vabs(ue1)), vabs(ve2)), gamma(6))
+    pdf_pos = f32(f32(1) / L["area"])
+    wl = cosine_hemisphere(*u1)
+    pdf_dir = f32(wl[2] * INV_PI)
+    v1, v2 = coordinate_system(L["n"])
+    w = add(add(mul(v1, wl[0]), mul(v2, wl[1])), mul(L["n"], wl[2]))
+    o = offset_origin(p, perr, L["n"], w)
+    Le = sc.Le if dot(L["n"], w) > 0 else (f32(0),) * 3
+    if pdf_pos == 0 or pdf_dir == 0 or all(x == 0 for x in Le):
+        return out
+    ad = f32(abs(dot(L["n"], w)))
+    den = f32(f32(f32(1) * pdf_pos) * pdf_dir)
+    beta = tuple(f32(f32(ad * x) / den) for x in Le)
+    if all(x == 0 for x in beta):
+        return out
+
+    def rec(o, d, depth, beta):
+        while depth < max_depth:
+            hit, tmax = sc.intersect(o, d)
+            if hit is None:
+                return
+            scattered = False
+            if sc.medium:
+                ch = min(int(f32(rng.uniform() * f32(3))), 2)
+                dist = f32(-logf(f32(f32(1) - rng.uniform())) / sc.sigma_t[ch])
+                dl = f32(dist * length(d))
+                t = tmax if tmax < dl else dl
+                scattered = bool(t < tmax)
+            if all(x == 0 for x in beta):
+                return
+            if scattered:
+                hx, hy = rng.get2d()
+                wi = hg_sample(sc.g, tuple(-x for x in d), hx, hy)
+                trv = sc.tr(d, tmax)
+                rec(add(o, mul(d, t)), wi, depth + 1, tuple(f32(b * x) for b, x in zip(beta, trv)))
+            bm = sc.tr(d, tmax) if sc.medium else (f32(1),) * 3
+            out.append((o, hit[0], f32(radius), tuple(f32(a * b) for a, b in zip(bm, beta))))
+            q = sc.quads[hit[2]]
+            ux, uy = rng.get2d()
+            if all(x == 0 for x in q["kd"]):
+                return
+            wo = tuple(-x for x in d)
+            woz = dot(wo, q["n"])
+            if woz == 0:
+                return
+            wil = list(cosine_hemisphere(ux, uy))
+            if woz < 0:
+                wil[2] = f32(wil[2] * f32(-1))
+            pdf = f32(abs(wil[2]) * INV_PI) if f32(woz * wil[2]) > 0 else f32(0)
+            fr = tuple(f32(k * INV_PI) for k in q["kd"])
+            if pdf == 0 or all(x == 0 for x in fr):
+                return
+            ss, ts, n = q["ss"], q["ts"], q["n"]
+            wi = tuple(f32(f32(f32(ss[i] * wil[0]) + f32(ts[i] * wil[1])) + f32(n[i] * wil[2])) for i in range(3))
+            adw = f32(abs(dot(wi, n)))
+            bn = tuple(f32(f32(f32(f32(bm[c] * beta[c]) * fr[c]) * adw) / pdf) for c in range(3))
+            o = offset_origin(hit[0], hit[1], n, wi)
+            d = wi
+
+            def y(s):
+                return f32(f32(f32(f32(0.212671) * s[0]) + f32(f32(0.715160) * s[1])) + f32(f32(0.072169) * s[2]))
+
+            ratio = f32(f32(1) - f32(y(bn) / y(beta)))
+            qrr = ratio if f32(0) < ratio else f32(0)
+            if rng.uniform() < qrr:
+                return
+            beta = tuple(f32(x / f32(f32(1) - qrr)) for x in bn)
+            depth += 1
+
+    rec(o, w, 0, beta)
+    return out
+
+
+def trace_photons(scene_struct, n_photons, iteration=0, max_depth=5, radius=0.01, first=None):
+    """Photons [0, first or n_photons) of a pass of n_photons (sequences iteration*N + i + 1)."""
+    sc = Scene(scene_struct)
+    beams = []
+    counts = []
+    for i in range(first if first is not None else n_photons):
+        b = trace_photon(sc, iteration * n_photons + i + 1, max_depth, radius)
+        counts.append(len(b))
+        beams.extend(b)
+    n = len(beams)
+    arr = {"start": np.zeros((n, 3), np.float32), "end": np.zeros((n, 3), np.float32),
+           "radius": np.zeros(n, np.float32), "power": np.zeros((n, 3), np.float32)}
+    for k, (s, e, r, pw) in enumerate(beams):
+        arr["start"][k] = s
+        arr["end"][k] = e
+        arr["radius"][k] = r
+        arr["power"][k] = pw
+    arr["counts"] = np.array(counts, np.int32)
+    return arr
+
+
+del math

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    txt = open(os.path.join(ROOT, "include", "bre.h")).read()
+    txt = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("bre.h", "bre_scene.h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(bre_[a-z_]+)\s*\(", txt)))
 

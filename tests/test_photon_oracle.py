@@ -1,0 +1,217 @@
+"""CPU tests of the photon-pass restatement (oracle/bre_oracle_photon.cpp) and its primitives.
+
+Pins, in order of strength:
+* PCG32: the published test vector of the PCG reference implementation (pcg32_srandom(42, 54));
+* Henyey-Greenstein: the reference's own tests, src/tests/hg.cpp:10-81, restated (sampling
+  consistent with p, orientation for g = +-0.95, normalisation);
+* include/bre_fmath.h against float64 numpy (<= 2 ulp), and bit-for-bit against a float32 Python
+  transliteration (tests/refpy_photon.py);
+* the whole photon pass against an independent pure-Python restatement (refpy_photon.py) for a
+  few hundred photons, bit for bit;
+* size-independent properties of the pass (determinism, 2^maxdepth - 1 bound, vacuum paths).
+The photon pass itself has no reference fixture: parity unpinned beyond these.
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+
+import refpy_photon as rp
+
+
+@pytest.fixture(scope="module")
+def scene_mod():
+    return importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
+
+
+# ---------------- PCG32 ----------------
+def test_pcg32_published_vector(oracle):
+    # pcg32-demo (pcg-random.org), pcg32_srandom_r(&rng, 42u, 54u)
+    want = [0xA15C02B7, 0x7B47F409, 0xBA1D3330, 0x83D2F293, 0xBFA4784B, 0xCBED606E]
+    assert oracle.pcg32_srandom(42, 54, 6).tolist() == want
+
+
+def test_pcg32_pbrt_seeding_and_float(oracle):
+    for seq in (1, 2, 1_000_001, 2**40 + 7):
+        r = rp.RNG(seq)
+        ints = [r.u32() for _ in range(64)]
+        assert oracle.pcg32(seq, 64).tolist() == ints
+        r = rp.RNG(seq)
+        fl = np.array([r.uniform() for _ in range(64)], np.float32)
+        got = oracle.pcg32(seq, 64, as_float=True)
+        assert np.array_equal(got.view(np.uint32), fl.view(np.uint32))
+        assert np.all(got < 1) and np.all(got >= 0)
+
+
+# ---------------- transcendentals ----------------
+def _ulp_err(y, ref):
+    ref32 = ref.astype(np.float32)
+    ulp = np.spacing(np.abs(ref32)).astype(np.float64)
+    return np.abs(y.astype(np.float64) - ref) / ulp
+
+
+def test_fmath_accuracy(oracle):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(1e-7, 1, 20000), rng.uniform(1, 100, 5000), 10.0 ** rng.uniform(-37, 30, 5000),
+                        [1.0, 0.5, 2.0, np.float32(1e-40), np.float32(1.17549435e-38)]]).astype(np.float32)
+    assert _ulp_err(oracle.fmath("log", x), np.log(x.astype(np.float64))).max() <= 2.0
+    x = np.concatenate([rng.uniform(-87, 88, 20000), rng.uniform(-2, 2, 10000), [0.0, -0.0, 1.0]]).astype(np.float32)
+    assert _ulp_err(oracle.fmath("exp", x), np.exp(x.astype(np.float64))).max() <= 2.0
+    x = rng.uniform(-7, 7, 30000).astype(np.float32)
+    x64 = x.astype(np.float64)
+    s, c = oracle.fmath("sin", x), oracle.fmath("cos", x)
+    # absolute bound near zeros of sin/cos, 2 ulp elsewhere
+    for got, ref in ((s, np.sin(x64)), (c, np.cos(x64))):
+        big = np.abs(ref) > 1e-3
+        assert _ulp_err(got[big], ref[big]).max() <= 2.0
+        assert np.abs(got[~big] - ref[~big]).max() <= 1e-9
+
+
+def test_fmath_edges(oracle):
+    assert oracle.fmath("log", np.array([0.0], np.float32))[0] == -np.inf
+    assert np.isnan(oracle.fmath("log", np.array([-1.0], np.float32))[0])
+    assert oracle.fmath("log", np.array([1.0], np.float32))[0] == 0.0
+    assert oracle.fmath("exp", np.array([0.0], np.float32))[0] == 1.0
+    assert oracle.fmath("exp", np.array([-200.0], np.float32))[0] == 0.0
+    assert oracle.fmath("exp", np.array([100.0], np.float32))[0] == np.inf
+    e = oracle.fmath("exp", np.array([-100.0], np.float32))[0]  # subnormal result
+    assert 0 < e < 1.2e-38 and abs(float(e) - float(np.float32(np.exp(-100.0)))) <= 1.5e-45  # 1 subnormal ulp
+
+
+def test_fmath_matches_python_transliteration(oracle):
+    rng = np.random.default_rng(11)
+    xl = rng.uniform(1e-6, 1.0, 300).astype(np.float32)
+    xe = rng.uniform(-30, 5, 300).astype(np.float32)
+    xs = rng.uniform(-3.2, 7.0, 300).astype(np.float32)
+    assert np.array_equal(oracle.fmath("log", xl), np.array([rp.logf(v) for v in xl], np.float32))
+    assert np.array_equal(oracle.fmath("exp", xe), np.array([rp.expf(v) for v in xe], np.float32))
+    assert np.array_equal(oracle.fmath("sin", xs), np.array([rp.sincosf(v)[0] for v in xs], np.float32))
+    assert np.array_equal(oracle.fmath("cos", xs), np.array([rp.sincosf(v)[1] for v in xs], np.float32))
+
+
+# ---------------- Henyey-Greenstein: src/tests/hg.cpp restated ----------------
+def _uniform_sphere(u):
+    z = 1 - 2 * u[:, 0]
+    r = np.sqrt(np.maximum(0, 1 - z * z))
+    phi = 2 * np.pi * u[:, 1]
+    return np.stack([r * np.cos(phi), r * np.sin(phi), z], axis=1).astype(np.float32)
+
+
+def test_hg_sampling_match(oracle):  # hg.cpp:10-24
+    rng = np.random.default_rng(0)
+    for g in np.arange(-0.75, 0.76, 0.25, dtype=np.float32):
+        wo = _uniform_sphere(rng.random((100, 2)))
+        u = rng.random((100, 2)).astype(np.float32)
+        wi, p0 = oracle.hg_sample(g, wo, u)
+        assert np.allclose(p0, oracle.hg_p(g, wo, wi), atol=1e-4), g
+
+
+@pytest.mark.parametrize("g,forward", [(0.95, True), (-0.95, False)])
+def test_hg_sampling_orientation(oracle, g, forward):  # hg.cpp:26-61
+    rng = np.random.default_rng(1)
+    wo = np.tile(np.array([[-1, 0, 0]], np.float32), (100, 1))
+    wi, _ = oracle.hg_sample(g, wo, rng.random((100, 2)).astype(np.float32))
+    nf, nb = int((wi[:, 0] > 0).sum()), int((wi[:, 0] <= 0).sum())
+    assert (nf >= 10 * nb) if forward else (nb >= 10 * nf)
+
+
+def test_hg_normalized(oracle):  # hg.cpp:63-81 (10x the samples: the 1e-3 bound is ~1 sigma at g=0.75)
+    rng = np.random.default_rng(2)
+    for g in np.arange(-0.75, 0.76, 0.25, dtype=np.float32):
+        wo = np.tile(_uniform_sphere(rng.random((1, 2))), (1000000, 1))
+        wi = _uniform_sphere(rng.random((1000000, 2)))
+        assert abs(oracle.hg_p(g, wo, wi).astype(np.float64).mean() - 1 / (4 * np.pi)) < 1e-3
+
+
+def test_hg_sample_unit_and_python(oracle):
+    rng = np.random.default_rng(4)
+    wo = _uniform_sphere(rng.random((200, 2)))
+    u = rng.random((200, 2)).astype(np.float32)
+    for g in (0.0, 0.0005, 0.7, -0.3):
+        wi, _ = oracle.hg_sample(g, wo, u)
+        assert np.allclose(np.linalg.norm(wi, axis=1), 1, atol=2e-6)
+        ref = np.array([rp.hg_sample(g, tuple(w), a, b) for w, (a, b) in zip(wo, u)], np.float32)
+        assert np.array_equal(wi, ref)
+
+
+# ---------------- medium and sampling primitives ----------------
+def test_homogeneous_tr(oracle):
+    rng = np.random.default_rng(5)
+    d = _uniform_sphere(rng.random((1000, 2))) * rng.uniform(0.5, 2, (1000, 1)).astype(np.float32)
+    t = rng.uniform(0, 5, 1000).astype(np.float32)
+    sa, ss = np.array([0.05, 0.1, 0.0], np.float32), np.array([0.5, 0.2, 1.0], np.float32)
+    tr = oracle.homogeneous_tr(sa, ss, d, t)
+    want = np.exp(-(sa + ss).astype(np.float64)[None, :] * (t.astype(np.float64) * np.linalg.norm(d, axis=1))[:, None])
+    assert np.allclose(tr, want, rtol=3e-6, atol=0)
+    # infinite segment: transmittance 0 (min(tMax*|d|, MaxFloat))
+    tr = oracle.homogeneous_tr(sa, ss, np.array([[1, 0, 0]], np.float32), np.array([np.inf], np.float32))
+    assert np.array_equal(tr, np.zeros((1, 3), np.float32))
+
+
+def test_cosine_hemisphere(oracle):
+    rng = np.random.default_rng(6)
+    u = rng.random((200000, 2)).astype(np.float32)
+    w = oracle.cosine_hemisphere(u)
+    assert np.allclose(np.linalg.norm(w, axis=1), 1, atol=2e-6) and np.all(w[:, 2] >= 0)
+    assert abs(w[:, 2].astype(np.float64).mean() - 2 / 3) < 3e-3  # E[cos] under cos/pi
+    assert np.array_equal(oracle.cosine_hemisphere(np.array([[0.5, 0.5]], np.float32)),
+                          np.array([[0, 0, 1]], np.float32))
+    ref = np.array([rp.cosine_hemisphere(a, b) for a, b in u[:300]], np.float32)
+    assert np.array_equal(w[:300], ref)
+
+
+# ---------------- the photon pass ----------------
+def test_scene_struct_matches_library(bre, scene_mod):
+    """scene.cornell_scene (Python) and bre_scene_cornell (libbre, host code) are the same bytes."""
+    lib = bre.load_library()
+    s = scene_mod.Scene()
+    lib.bre_scene_cornell(ctypes.addressof(s), 0.05, 0.5, 0.0)
+    assert s.to_bytes() == scene_mod.cornell_scene(0.05, 0.5, 0.0).to_bytes()
+
+
+@pytest.mark.parametrize("kw,depth,it", [(dict(), 5, 0), (dict(g=0.7), 5, 3), (dict(g=-0.5, sigma_s=2.0), 8, 1),
+                                         (dict(sigma_a=0.0, sigma_s=0.0), 5, 0)])
+def test_oracle_matches_python_restatement(oracle, scene_mod, kw, depth, it):
+    s = scene_mod.cornell_scene(**kw)
+    n, k = 5000, 150
+    ref = oracle.trace_photons(s, n, iteration=it, max_depth=depth)
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        py = rp.trace_photons(s, n, iteration=it, max_depth=depth, first=k)
+    assert np.array_equal(ref["counts"][:k], py["counts"])
+    nb = int(py["counts"].sum())
+    for key in ("start", "end", "radius", "power"):
+        assert np.array_equal(ref[key][:nb].view(np.uint32), py[key].view(np.uint32)), key
+
+
+def test_photon_pass_properties(oracle, scene_mod):
+    s = scene_mod.cornell_scene()
+    a = oracle.trace_photons(s, 20000, max_depth=5)
+    b = oracle.trace_photons(s, 20000, max_depth=5)
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    assert a["counts"].max() <= 31 and a["counts"].sum() == a["radius"].shape[0]
+    for k in ("start", "end"):
+        assert np.all(a[k] >= -1e-4) and np.all(a[k] <= 1 + 1e-4)
+    assert np.all(np.isfinite(a["power"])) and np.all(a["power"] >= 0)
+    # other iterations use other sequences
+    c = oracle.trace_photons(s, 20000, iteration=1, max_depth=5)
+    assert not np.array_equal(a["end"][:100], c["end"][:100])
+    # the first beam of a photon that did not scatter starts on the light (y just below 0.999)
+    first = np.concatenate([[0], np.cumsum(a["counts"])[:-1]])[a["counts"] == 1]
+    assert np.all(np.abs(a["start"][first, 1] - 0.999) < 1e-5)
+
+
+def test_photon_pass_vacuum_and_depth(oracle, scene_mod):
+    vac = scene_mod.make_scene(scene_mod.cornell_quads(), 6, (17.0, 12.0, 4.0))
+    a = oracle.trace_photons(vac, 5000, max_depth=5)
+    assert a["counts"].max() <= 5
+    # vacuum: beam k+1 starts where beam k ended (up to the surface offset)
+    idx = np.concatenate([[0], np.cumsum(a["counts"])])
+    for i in range(200):
+        s0, s1 = idx[i], idx[i + 1]
+        if s1 - s0 > 1:
+            assert np.allclose(a["start"][s0 + 1:s1], a["end"][s0:s1 - 1], atol=1e-5)
+    # with no medium the power at the end is beta itself: it only decreases through bounces / RR
+    # renormalisation keeps luminance-weighted power constant when RR continues
+    d1 = oracle.trace_photons(scene_mod.cornell_scene(), 5000, max_depth=1)
+    assert d1["counts"].max() <= 1
