@@ -30,6 +30,7 @@ EXPORTS = [
     "bre_set_stream", "bre_synchronize", "bre_get_stats", "bre_set_beams",
     "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
     "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell",
+    "bre_camera_pass", "bre_gather_camera", "bre_get_segments", "bre_render_iteration", "bre_render",
 ]
 
 
@@ -50,7 +51,9 @@ class Stats(ctypes.Structure):
                 ("build_ms", ctypes.c_double),
                 ("gather_ms", ctypes.c_double),
                 ("n_photons", ctypes.c_int64),
-                ("photon_ms", ctypes.c_double)]
+                ("photon_ms", ctypes.c_double),
+                ("n_camera_segments", ctypes.c_int64),
+                ("camera_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -108,6 +111,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_get_beams.restype = I32
     lib.bre_scene_cornell.argtypes = [P, F, F, F]
     lib.bre_scene_cornell.restype = None
+    lib.bre_camera_pass.argtypes = [P, P, I32, I32, I32, I32, I32, I32, P, ctypes.POINTER(I64)]
+    lib.bre_camera_pass.restype = I32
+    lib.bre_gather_camera.argtypes = [P, F, P]
+    lib.bre_gather_camera.restype = I32
+    lib.bre_get_segments.argtypes = [P, I64, P, P, P, P, P, P, ctypes.POINTER(I64)]
+    lib.bre_get_segments.restype = I32
+    lib.bre_render_iteration.argtypes = [P, P, P, I32, P]
+    lib.bre_render_iteration.restype = I32
+    lib.bre_render.argtypes = [P, P, P, P]
+    lib.bre_render.restype = I32
     _LIB = lib
     return lib
 
@@ -204,6 +217,43 @@ class BeamGather:
         self._check(self.lib.bre_get_beams(self.h, n, _ptr(out["start"]), _ptr(out["end"]), _ptr(out["radius"]),
                                            _ptr(out["power"]), ctypes.byref(nb)))
         return out
+
+    # ---- camera pass ----
+    def camera_pass(self, scene, width: int, height: int, iteration: int = 0, max_depth: int = 5,
+                    render_surfaces: bool = True, render_media: bool = True, surface=None) -> int:
+        """Camera pass on the GPU (photonbeam.cpp:444-555).  `surface`: optional torch float32
+        CUDA tensor (W*H, 3) receiving += the surface radiance.  Returns the segment count."""
+        n = ctypes.c_int64(0)
+        self._check(self.lib.bre_camera_pass(self.h, ctypes.addressof(scene), int(width), int(height),
+                                             int(iteration), int(max_depth), int(render_surfaces),
+                                             int(render_media), _ptr(surface), ctypes.byref(n)))
+        return n.value
+
+    def gather_camera(self, R: float, accum):
+        """Gather the last camera pass's segments into `accum` (torch CUDA tensor (W*H, 3))."""
+        self._check(self.lib.bre_gather_camera(self.h, float(R), _ptr(accum)))
+
+    def get_segments(self):
+        n = ctypes.c_int64(0)
+        self._check(self.lib.bre_get_segments(self.h, 0, None, None, None, None, None, None, ctypes.byref(n)))
+        k = n.value
+        out = {"o": np.zeros((k, 3), np.float32), "p": np.zeros((k, 3), np.float32), "d": np.zeros((k, 3), np.float32),
+               "tmax": np.zeros(k, np.float32), "pixel": np.zeros(k, np.int32), "depth": np.zeros(k, np.int32)}
+        self._check(self.lib.bre_get_segments(self.h, k, _ptr(out["o"]), _ptr(out["p"]), _ptr(out["d"]),
+                                              _ptr(out["tmax"]), _ptr(out["pixel"]), _ptr(out["depth"]),
+                                              ctypes.byref(n)))
+        return out
+
+    # ---- the integrator ----
+    def render_iteration(self, scene, params, iteration: int, ld):
+        self._check(self.lib.bre_render_iteration(self.h, ctypes.addressof(scene), ctypes.addressof(params),
+                                                  int(iteration), _ptr(ld)))
+
+    def render(self, scene, params):
+        """Whole PhotonBeamIntegrator::Render; returns the (H, W, 3) float32 image Ld / end_iteration."""
+        img = np.zeros((params.height, params.width, 3), np.float32)
+        self._check(self.lib.bre_render(self.h, ctypes.addressof(scene), ctypes.addressof(params), _ptr(img)))
+        return img
 
     # ---- gather ----
     def gather(self, o, p, d, tmax, pixel=None, R=0.01, npix=0, accum=None, seg_rgb=True, counts=False):

@@ -71,6 +71,13 @@ struct bre_ctx {
     DevMem counters_buf, roots, partial, pcnt, redo;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp;
+    // camera pass
+    DevMem cam_dev, cam_perms, cs_o, cs_p, cs_d, cs_t, cs_pix, cs_valid, cam_offs, cam_tmp, cam_flags;
+    DevMem seg_o, seg_p, seg_d, seg_t, seg_pix, seg_depth;
+    int64_t cam_nseg = 0;
+    int64_t cam_npix = 0;
+    int cam_w = -1, cam_h = -1;  // film the Halton / camera tables were prepared for
+    bre_scene cam_scene;         // scene the camera tables were prepared for
     bool beams_kept = false;  // in_* hold the current beam set (bre_get_beams)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bre_stats stats;
@@ -277,6 +284,12 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     return BRE_OK;
 }
 
+// exclusive scan of the camera slots' valid flags into cam_offs
+hipError_t rocprim_free_total_scan(bre_ctx *c, const CamSlots &cs, int64_t nslots, int max_depth) {
+    return launch_camera_scan(c->cam_tmp.ptr, c->cam_tmp.cap, cs, nslots, max_depth, c->cam_offs.as<int64_t>(),
+                              c->stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -315,7 +328,10 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo,
-                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp};
+                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->cam_dev, &c->cam_perms,
+                     &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
+                     &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
+                     &c->seg_depth};
     for (DevMem *m : all) m->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -438,7 +454,7 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     DevScene hs;
-    prepare_scene(scene, 0, 0, &hs);
+    prepare_scene(scene, &hs);
     const size_t N = (size_t)n_photons;
     HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
     HIPCHK(c, c->ph_counts.ensure((N + 1) * sizeof(int32_t)));
@@ -504,6 +520,188 @@ bre_status bre_get_beams(bre_ctx *c, int64_t capacity, float *start, float *end,
     HIPCHK(c, hipMemcpyAsync(power, c->in_power.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BRE_OK;
+}
+
+static bre_status check_scene(bre_ctx *c, const bre_scene *scene, const char *fn) {
+    if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "%s: null scene", fn);
+    if (scene->n_quads < 1 || scene->n_quads > BRE_MAX_QUADS || scene->light_quad < 0 ||
+        scene->light_quad >= scene->n_quads)
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: bad quad count or light index", fn);
+    return BRE_OK;
+}
+
+bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, int32_t height, int32_t iteration,
+                           int32_t max_depth, int32_t render_surfaces, int32_t render_media, float *d_surface,
+                           int64_t *n_segments) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (n_segments) *n_segments = 0;
+    bre_status st = check_scene(c, scene, "bre_camera_pass");
+    if (st != BRE_OK) return st;
+    if (width < 1 || height < 1 || (int64_t)width * height > (int64_t)INT32_MAX / BRE_MAX_DEPTH || iteration < 0)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_camera_pass: bad film size or iteration");
+    if (max_depth < 1 || max_depth > BRE_MAX_DEPTH)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_camera_pass: max_depth must be in [1, %d]", BRE_MAX_DEPTH);
+    st = set_device(c);
+    if (st != BRE_OK) return st;
+    // scene + camera/Halton tables (rebuilt when the scene or film changes)
+    DevScene hs;
+    prepare_scene(scene, &hs);
+    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
+    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    if (c->cam_w != width || c->cam_h != height || memcmp(&c->cam_scene, scene, sizeof(bre_scene)) != 0) {
+        DevCamera cam;
+        std::vector<uint16_t> perms;
+        prepare_camera(scene, width, height, &cam, &perms);
+        HIPCHK(c, c->cam_dev.ensure(sizeof(DevCamera)));
+        HIPCHK(c, c->cam_perms.ensure(perms.size() * sizeof(uint16_t)));
+        HIPCHK(c, hipMemcpyAsync(c->cam_dev.ptr, &cam, sizeof(cam), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->cam_perms.ptr, perms.data(), perms.size() * sizeof(uint16_t),
+                                 hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors go out of scope
+        c->cam_w = width;
+        c->cam_h = height;
+        memcpy(&c->cam_scene, scene, sizeof(bre_scene));
+    }
+    const int64_t nslots = camera_slots(width, height);
+    const size_t S = (size_t)(nslots * max_depth);
+    HIPCHK(c, c->cs_o.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->cs_p.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->cs_d.ensure(S * 3 * sizeof(float)));
+    HIPCHK(c, c->cs_t.ensure(S * sizeof(float)));
+    HIPCHK(c, c->cs_pix.ensure(S * sizeof(int32_t)));
+    HIPCHK(c, c->cs_valid.ensure(S * sizeof(int32_t)));
+    HIPCHK(c, c->cam_offs.ensure((S + 1) * sizeof(int64_t)));
+    const size_t tmp = camera_scan_temp_bytes((int64_t)S);
+    HIPCHK(c, c->cam_tmp.ensure(tmp + 16));
+    HIPCHK(c, c->cam_flags.ensure(sizeof(unsigned int)));
+    HIPCHK(c, hipMemsetAsync(c->cam_flags.ptr, 0, sizeof(unsigned int), c->stream));
+    CamSlots cs{c->cs_o.as<float>(), c->cs_p.as<float>(), c->cs_d.as<float>(), c->cs_t.as<float>(),
+                c->cs_pix.as<int32_t>(), c->cs_valid.as<int32_t>()};
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->cam_dev.as<DevCamera>(), c->cam_perms.as<uint16_t>(),
+                            width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
+                            c->cam_flags.as<unsigned int>(), c->stream));
+    // total = offs[S-1] + valid[S-1]
+    HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
+    int64_t last_off = 0;
+    int32_t last_valid = 0;
+    unsigned int flags = 0;
+    HIPCHK(c, hipMemcpyAsync(&last_off, c->cam_offs.as<int64_t>() + (S - 1), sizeof(int64_t), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(&last_valid, c->cs_valid.as<int32_t>() + (S - 1), sizeof(int32_t),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&flags, c->cam_flags.ptr, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (flags & 1u) return fail(c, BRE_ERR_STATE, "bre_camera_pass: a path needed more than %d Halton dimensions", kHaltonDims);
+    const int64_t n = last_off + last_valid;
+    const size_t N = (size_t)(n > 0 ? n : 1);
+    HIPCHK(c, c->seg_o.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->seg_p.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->seg_d.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->seg_t.ensure(N * sizeof(float)));
+    HIPCHK(c, c->seg_pix.ensure(N * sizeof(int32_t)));
+    HIPCHK(c, c->seg_depth.ensure(N * sizeof(int32_t)));
+    HIPCHK(c, launch_camera_compact(cs, nslots, max_depth, c->cam_offs.as<int64_t>(), c->seg_o.as<float>(),
+                                    c->seg_p.as<float>(), c->seg_d.as<float>(), c->seg_t.as<float>(),
+                                    c->seg_pix.as<int32_t>(), c->seg_depth.as<int32_t>(), c->stream));
+    float ms = 0.f;
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->cam_nseg = n;
+    c->cam_npix = (int64_t)width * height;
+    c->stats.n_camera_segments = n;
+    c->stats.camera_ms = ms;
+    if (n_segments) *n_segments = n;
+    return BRE_OK;
+}
+
+bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (c->cam_npix == 0) return fail(c, BRE_ERR_STATE, "bre_gather_camera: no camera pass yet");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    return gather_device(c, c->cam_nseg, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
+                         c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, nullptr, nullptr);
+}
+
+bre_status bre_get_segments(bre_ctx *c, int64_t capacity, float *o, float *p, float *d, float *tmax, int32_t *pixel,
+                            int32_t *depth, int64_t *n_segments) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (capacity < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_get_segments: negative capacity");
+    if (n_segments) *n_segments = c->cam_nseg;
+    const int64_t k = capacity < c->cam_nseg ? capacity : c->cam_nseg;
+    if (k <= 0) return BRE_OK;
+    if (!o || !p || !d || !tmax || !pixel || !depth)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_get_segments: null array");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    const size_t K = (size_t)k;
+    HIPCHK(c, hipMemcpyAsync(o, c->seg_o.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(p, c->seg_p.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d, c->seg_d.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(tmax, c->seg_t.ptr, K * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(pixel, c->seg_pix.ptr, K * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(depth, c->seg_depth.ptr, K * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
+static bre_status check_params(bre_ctx *c, const bre_render_params *rp) {
+    if (!rp) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null params");
+    if (rp->width < 1 || rp->height < 1 || rp->photons_per_iteration < 0 || rp->start_iteration < 0 ||
+        rp->end_iteration < rp->start_iteration || rp->max_depth < 1 || rp->max_depth > BRE_MAX_DEPTH)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_render: bad parameters");
+    return BRE_OK;
+}
+
+bre_status bre_render_iteration(bre_ctx *c, const bre_scene *scene, const bre_render_params *rp, int32_t iteration,
+                                float *d_ld) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    bre_status st = check_params(c, rp);
+    if (st != BRE_OK) return st;
+    if (!d_ld) return fail(c, BRE_ERR_INVALID_ARG, "bre_render_iteration: null Ld buffer");
+    const float R = bre_beam_radius_at(rp->initial_radius, rp->alpha, iteration);
+    st = bre_trace_photons(c, scene, rp->photons_per_iteration, iteration, rp->max_depth, R, nullptr);
+    if (st != BRE_OK) return st;
+    st = bre_camera_pass(c, scene, rp->width, rp->height, iteration, rp->max_depth, rp->render_surfaces,
+                         rp->render_media, d_ld, nullptr);
+    if (st != BRE_OK) return st;
+    if (rp->render_media) return bre_gather_camera(c, R, d_ld);
+    return BRE_OK;
+}
+
+bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_params *rp, float *image) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    bre_status st = check_params(c, rp);
+    if (st != BRE_OK) return st;
+    if (!image) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null image");
+    st = set_device(c);
+    if (st != BRE_OK) return st;
+    const int64_t npix = (int64_t)rp->width * rp->height;
+    float *ld = nullptr;
+    HIPCHK(c, hipMalloc(&ld, (size_t)npix * 3 * sizeof(float)));
+    st = BRE_OK;
+    if (hipMemsetAsync(ld, 0, (size_t)npix * 3 * sizeof(float), c->stream) != hipSuccess)
+        st = fail(c, BRE_ERR_HIP, "bre_render: memset failed");
+    for (int it = rp->start_iteration; st == BRE_OK && it < rp->end_iteration; ++it)
+        st = bre_render_iteration(c, scene, rp, it, ld);
+    if (st == BRE_OK) {
+        std::vector<float> h((size_t)npix * 3);
+        if (hipMemcpyAsync(h.data(), ld, h.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            st = fail(c, BRE_ERR_HIP, "bre_render: copy-back failed");
+        else if (rp->end_iteration > rp->start_iteration)
+            st = bre_resolve_image(npix, h.data(), rp->end_iteration - 1, image);  // Ld / (iter + 1)
+        else
+            memset(image, 0, h.size() * sizeof(float));
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(ld);
+    return st;
 }
 
 void bre_scene_cornell(bre_scene *s, float sigma_a, float sigma_s, float g) {

@@ -22,7 +22,7 @@
 
 namespace bre {
 
-void prepare_scene(const bre_scene *s, int width, int height, DevScene *out) {
+void prepare_scene(const bre_scene *s, DevScene *out) {
     DevScene d{};
     d.n_quads = s->n_quads;
     d.light = s->light_quad;
@@ -48,8 +48,6 @@ void prepare_scene(const bre_scene *s, int width, int height, DevScene *out) {
         for (int k = 0; k < 3; ++k) Q.kd[k] = q.kd[k];
         Q.absorb = (q.kd[0] == 0 && q.kd[1] == 0 && q.kd[2] == 0) ? 1 : 0;
     }
-    (void)width;
-    (void)height;
     *out = d;
 }
 

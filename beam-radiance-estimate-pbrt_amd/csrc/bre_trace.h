@@ -10,6 +10,8 @@
 #include "../../include/bre_scene.h"
 #include "bre_math.h"
 
+#include <vector>
+
 namespace bre {
 
 #define BRE_TD __host__ __device__ __forceinline__
@@ -153,37 +155,44 @@ struct DevScene {
     float Le[3];
     float sigma_t[3];
     float g;
-    // pinhole camera (perspective.cpp with lensradius 0): world-space frame and raster mapping
-    f3 cam_o, cam_x, cam_y, cam_z;
-    float cam_sx, cam_sy;  // screen window half-extents (tan(fov/2) * aspect terms)
     PQuad q[BRE_MAX_QUADS];
 };
 
-// host: derive per-quad constants exactly as oracle/bre_oracle_photon.cpp make_scene does
-void prepare_scene(const bre_scene *s, int width, int height, DevScene *out);
+// host: derive per-quad constants exactly as oracle/ora_pbrt.h make_scene does
+void prepare_scene(const bre_scene *s, DevScene *out);
 
 struct Hit {
     f3 p, perr;
     int quad;
 };
 
+// one quad: plane solve, (u, v) in [0,1]^2, t in (0, tmax); hit point rebuilt on the quad with
+// the parallelogram form of the triangle error bound
+__device__ __forceinline__ bool intersect_quad(const PQuad &q, f3 o, f3 d, float tmax, float &t, Hit &h) {
+    const float denom = dot3(q.n, d);
+    if (denom == 0) return false;
+    t = dot3(q.n, sub3(q.p0, o)) / denom;
+    if (!(t > 0 && t < tmax)) return false;
+    const f3 rel = sub3(ray_at(o, d, t), q.p0);
+    const float u = dot3(rel, q.e1) * q.inv_e1sq;
+    const float v = dot3(rel, q.e2) * q.inv_e2sq;
+    if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) return false;
+    const f3 ue1 = scale3(q.e1, u), ve2 = scale3(q.e2, v);
+    h.p = add3(add3(q.p0, ue1), ve2);
+    h.perr = scale3(add3(add3(abs3(q.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
+    return true;
+}
+
 // closest hit over all quads; strict <, lowest index wins a tie; t in (0, tmax)
 __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, float &tmax, Hit &h) {
     bool hit = false;
     for (int i = 0; i < S.n_quads; ++i) {
-        const PQuad &q = S.q[i];
-        const float denom = dot3(q.n, d);
-        if (denom == 0) continue;
-        const float t = dot3(q.n, sub3(q.p0, o)) / denom;
-        if (!(t > 0 && t < tmax)) continue;
-        const f3 rel = sub3(ray_at(o, d, t), q.p0);
-        const float u = dot3(rel, q.e1) * q.inv_e1sq;
-        const float v = dot3(rel, q.e2) * q.inv_e2sq;
-        if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) continue;
+        float t;
+        Hit tmp;
+        if (!intersect_quad(S.q[i], o, d, tmax, t, tmp)) continue;
         tmax = t;
-        const f3 ue1 = scale3(q.e1, u), ve2 = scale3(q.e2, v);
-        h.p = add3(add3(q.p0, ue1), ve2);
-        h.perr = scale3(add3(add3(abs3(q.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
+        h.p = tmp.p;
+        h.perr = tmp.perr;
         h.quad = i;
         hit = true;
     }
@@ -208,6 +217,38 @@ __device__ __forceinline__ bool medium_sample(const DevScene &S, Pcg &rng, f3 d,
 
 BRE_TD bool black3(const float v[3]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
 BRE_TD float lum3(const float v[3]) { return 0.212671f * v[0] + 0.715160f * v[1] + 0.072169f * v[2]; }
+
+// ---- camera pass (bre_camera.hip) ----
+constexpr int kHaltonDims = 256;  // Halton dimensions with permutation tables (paths use <= 133)
+
+struct DevCamera {
+    f3 pos, dir, right, nup;           // LookAt frame
+    float sx0, sx1, sy0, sy1;          // screen window
+    float tan_ang, fw, fh;             // tan(fov/2), film size as float
+    int width, height;
+    int base_scale[2], base_exp[2];    // HaltonSampler baseScales / baseExponents
+    int stride;                        // sampleStride
+    int mult_inv[2];                   // multInverse
+    int primes[kHaltonDims];
+    int prime_sums[kHaltonDims];
+};
+
+// per-(depth, pixel-slot) camera segments before compaction
+struct CamSlots {
+    float *o, *p, *d, *t;
+    int32_t *pix, *valid;
+};
+
+void prepare_camera(const bre_scene *s, int width, int height, DevCamera *c, std::vector<uint16_t> *perms);
+int64_t camera_slots(int width, int height);
+hipError_t launch_camera(const DevScene *scene, const DevCamera *cam, const uint16_t *perms, int width, int height,
+                         int iteration, int max_depth, int render_surfaces, int render_media, const CamSlots &s,
+                         float *surface, unsigned int *flags, hipStream_t stream);
+size_t camera_scan_temp_bytes(int64_t n);
+hipError_t launch_camera_scan(void *tmp, size_t tmp_bytes, const CamSlots &s, int64_t nslots, int max_depth,
+                              int64_t *offs, hipStream_t stream);
+hipError_t launch_camera_compact(const CamSlots &s, int64_t nslots, int max_depth, const int64_t *offs, float *o,
+                                 float *p, float *d, float *t, int32_t *pix, int32_t *depth, hipStream_t stream);
 
 // photon pass launchers (bre_photon.hip)
 hipError_t launch_photons(const DevScene *scene, int64_t n, uint64_t seq0, int max_depth, float radius,

@@ -28,6 +28,23 @@ class Scene(ctypes.Structure):
         return ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self))
 
 
+class RenderParams(ctypes.Structure):
+    """bre_render_params: CreatePhotonBeamIntegrator's parameters (photonbeam.cpp:589-611)."""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("iterations", ctypes.c_int32),
+                ("start_iteration", ctypes.c_int32), ("end_iteration", ctypes.c_int32),
+                ("photons_per_iteration", ctypes.c_int64), ("max_depth", ctypes.c_int32),
+                ("render_surfaces", ctypes.c_int32), ("render_media", ctypes.c_int32),
+                ("initial_radius", ctypes.c_float), ("alpha", ctypes.c_float)]
+
+
+def render_params(width, height, iterations=64, photons=-1, max_depth=5, radius=1.0, alpha=0.5,
+                  render_surfaces=True, render_media=True, start_iteration=0, end_iteration=None) -> RenderParams:
+    """Defaults as the reference's (iterations 64, maxdepth 5, initialbeamradius 1, alpha 0.5)."""
+    return RenderParams(int(width), int(height), int(iterations), int(start_iteration),
+                        int(iterations if end_iteration is None else end_iteration), int(photons), int(max_depth),
+                        int(render_surfaces), int(render_media), float(radius), float(alpha))
+
+
 def _f3(v):
     return F3(*[float(x) for x in v])
 

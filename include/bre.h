@@ -95,6 +95,8 @@ typedef struct bre_stats {
     double gather_ms;        /* device time of the last gather kernel (timing only) */
     int64_t n_photons;       /* photons traced by the last bre_trace_photons */
     double photon_ms;        /* device time of the last photon pass, both passes (timing only) */
+    int64_t n_camera_segments; /* segments of the last bre_camera_pass */
+    double camera_ms;        /* device time of the last camera pass incl. compaction (timing only) */
 } bre_stats;
 
 /* ---- context ---- */
@@ -153,6 +155,35 @@ bre_status bre_trace_photons(bre_ctx *ctx, const bre_scene *scene, int64_t n_pho
    BRE_ERR_STATE after bre_set_beams_device (the library keeps no copy of caller device arrays). */
 bre_status bre_get_beams(bre_ctx *ctx, int64_t capacity, float *start_xyz, float *end_xyz, float *radius,
                          float *power_end_rgb, int64_t *n_beams);
+
+/* ---- camera pass (replaces photonbeam.cpp:444-555 up to the gather) ----
+   Walks one camera path per pixel of a width x height film for `iteration` on the device
+   (HaltonSampler sample `iteration` of each pixel, perspective pinhole, scene intersection,
+   homogeneous-medium transmittance, Lambertian bounces and Russian roulette) and keeps the
+   segment [ray.o, isect.p] of every surface-hit camera ray in the context: depth-major, pixels in
+   8x8-tile order within a depth.  d_surface_rgb (device float[3*W*H], may be NULL) receives += the
+   surface radiance of rendersurfaces (emission seen directly + UniformSampleOneLight).  max_depth
+   in [1, BRE_MAX_DEPTH].  *n_segments (may be NULL) receives the segment count.  Synchronous. */
+bre_status bre_camera_pass(bre_ctx *ctx, const bre_scene *scene, int32_t width, int32_t height, int32_t iteration,
+                           int32_t max_depth, int32_t render_surfaces, int32_t render_media, float *d_surface_rgb,
+                           int64_t *n_segments);
+/* Gather the context's camera segments against its beam set: bre_gather_device on them, adding
+   into d_accum_rgb (device float[3*W*H] of the last camera pass).  Asynchronous. */
+bre_status bre_gather_camera(bre_ctx *ctx, float beam_radius_cur, float *d_accum_rgb);
+/* Copy the camera segments back (tests): xyz arrays, tmax, pixel index and path depth. */
+bre_status bre_get_segments(bre_ctx *ctx, int64_t capacity, float *o_xyz, float *p_xyz, float *d_xyz, float *tmax,
+                            int32_t *pixel, int32_t *depth, int64_t *n_segments);
+
+/* ---- the integrator (PhotonBeamIntegrator::Render, photonbeam.cpp:329-586) ----
+   For iteration in [start_iteration, end_iteration): photon pass (bre_trace_photons) with the
+   iteration's radius R_i, BVH build, camera pass, gather of every segment with R_i into the
+   per-pixel Ld (device, float[3*W*H], accumulated across calls: the caller zeroes it once), then
+   R_{i+1} = R_i (i + alpha) / (i + 1).  bre_render_iteration runs one iteration on caller device
+   memory; bre_render runs the whole range and writes L = Ld / end_iteration (the image the
+   reference hands to Film::SetImage at its last write, :565-583) to host image_rgb[3*W*H]. */
+bre_status bre_render_iteration(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params,
+                                int32_t iteration, float *d_ld_rgb);
+bre_status bre_render(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params, float *image_rgb);
 
 /* ---- integrator helpers (photonbeam.cpp:354-356, 562, 578) ---- */
 /* R_i for iteration i: R_{k+1} = R_k * (k + alpha) / (k + 1), R_0 = initial, in float. */

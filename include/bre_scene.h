@@ -57,6 +57,20 @@ typedef struct bre_scene {
     bre_quad quads[BRE_MAX_QUADS];
 } bre_scene;
 
+/* PhotonBeamIntegrator parameters (CreatePhotonBeamIntegrator, photonbeam.cpp:589-611). */
+typedef struct bre_render_params {
+    int32_t width, height;          /* film resolution (pixelBounds = [0,W) x [0,H)) */
+    int32_t iterations;             /* "iterations" (default 64) */
+    int32_t start_iteration;        /* "startiteration" (default 0) */
+    int32_t end_iteration;          /* "enditeration" (default = iterations) */
+    int64_t photons_per_iteration;  /* "photonsperiteration" */
+    int32_t max_depth;              /* "maxdepth" (default 5) */
+    int32_t render_surfaces;        /* "rendersurfaces" (default 1) */
+    int32_t render_media;           /* "rendermedia" (default 1) */
+    float initial_radius;           /* "initialbeamradius" (default 1) */
+    float alpha;                    /* "alpha" (default 0.5) */
+} bre_render_params;
+
 /* The benchmark scene of SURVEY.md §8d (C1/C2): unit-cube Cornell box (white floor, ceiling and
    back wall, red left wall, green right wall, white front wall behind the camera), a 0.3 x 0.3
    area light just below the ceiling facing down, homogeneous fog sigma_a, sigma_s (grey), HG g,

@@ -1,0 +1,318 @@
+// ora_pbrt.h — pbrt building blocks restated for the oracle's photon and camera passes
+// (TEST INFRASTRUCTURE; see bre_oracle_photon.cpp for the file:line list and interpretation notes).
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../include/bre_fmath.h"
+#include "../include/bre_scene.h"
+
+namespace orp {
+
+typedef float Float;
+static const Float Pi = 3.14159265358979323846f;
+static const Float InvPi = 0.31830988618379067154f;
+static const Float Inv4Pi = 0.07957747154594766788f;
+static const Float PiOver2 = 1.57079632679489661923f;
+static const Float PiOver4 = 0.78539816339744830961f;
+static const Float OneMinusEpsilon = 0x1.fffffep-1f;
+static const Float MachineEpsilon = 0x1p-24f;
+static const Float Infinity = __builtin_huge_valf();
+static const Float MaxFloat = 3.402823466e+38f;
+
+static inline Float gamma(int n) { return (n * MachineEpsilon) / (1 - n * MachineEpsilon); }
+
+// ---- RNG (rng.h:60-144) ----
+struct RNG {
+    uint64_t state, inc;
+    RNG() : state(0x853c49e6748fea9bULL), inc(0xda3e39cb94b95bdbULL) {}  // PCG32_DEFAULT_STATE/STREAM
+    explicit RNG(uint64_t seq) { SetSequence(seq); }
+    uint32_t UniformUInt32(uint32_t b) {
+        uint32_t threshold = (~b + 1u) % b;
+        while (true) {
+            uint32_t r = UniformUInt32();
+            if (r >= threshold) return r % b;
+        }
+    }
+    void SetSequence(uint64_t initseq) {
+        state = 0u;
+        inc = (initseq << 1u) | 1u;
+        UniformUInt32();
+        state += 0x853c49e6748fea9bULL;
+        UniformUInt32();
+    }
+    uint32_t UniformUInt32() {
+        uint64_t oldstate = state;
+        state = oldstate * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xorshifted = (uint32_t)(((oldstate >> 18u) ^ oldstate) >> 27u);
+        uint32_t rot = (uint32_t)(oldstate >> 59u);
+        return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+    }
+    Float UniformFloat() {
+        return std::min(OneMinusEpsilon, Float(UniformUInt32() * 0x1p-32f));
+    }
+};
+
+// AwesomeHaltonSampler past its 1000 Halton dimensions (photonbeam.cpp:226-256)
+struct Sampler {
+    RNG rng;
+    explicit Sampler(uint64_t seq) : rng(seq) {}
+    Float Get1D() { return rng.UniformFloat(); }
+    void Get2D(Float *x, Float *y) {
+        Float first = Get1D();
+        Float second = Get1D();
+        *x = second;  // g++ evaluates Point2f(Get1D(), Get1D()) right to left
+        *y = first;
+    }
+};
+
+// ---- geometry (geometry.h) ----
+struct V3 {
+    Float x, y, z;
+    V3() : x(0), y(0), z(0) {}
+    V3(Float a, Float b, Float c) : x(a), y(b), z(c) {}
+    explicit V3(const float *p) : x(p[0]), y(p[1]), z(p[2]) {}
+    Float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    Float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+    V3 operator+(const V3 &b) const { return V3(x + b.x, y + b.y, z + b.z); }
+    V3 operator-(const V3 &b) const { return V3(x - b.x, y - b.y, z - b.z); }
+    V3 operator-() const { return V3(-x, -y, -z); }
+    V3 operator*(Float s) const { return V3(s * x, s * y, s * z); }
+    V3 operator/(Float f) const {
+        Float inv = (Float)1 / f;
+        return V3(x * inv, y * inv, z * inv);
+    }
+    Float LengthSquared() const { return x * x + y * y + z * z; }
+    Float Length() const { return std::sqrt(LengthSquared()); }
+};
+static inline V3 operator*(Float s, const V3 &v) { return v * s; }
+static inline Float Dot(const V3 &a, const V3 &b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline Float AbsDot(const V3 &a, const V3 &b) { return std::fabs(Dot(a, b)); }
+static inline V3 Abs(const V3 &a) { return V3(std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)); }
+static inline V3 Normalize(const V3 &v) { return v / v.Length(); }
+// Cross in double (geometry.h:957-963)
+static inline V3 Cross(const V3 &v1, const V3 &v2) {
+    double v1x = v1.x, v1y = v1.y, v1z = v1.z;
+    double v2x = v2.x, v2y = v2.y, v2z = v2.z;
+    return V3((Float)((v1y * v2z) - (v1z * v2y)), (Float)((v1z * v2x) - (v1x * v2z)),
+              (Float)((v1x * v2y) - (v1y * v2x)));
+}
+static inline void CoordinateSystem(const V3 &v1, V3 *v2, V3 *v3) {
+    if (std::fabs(v1.x) > std::fabs(v1.y))
+        *v2 = V3(-v1.z, 0, v1.x) / std::sqrt(v1.x * v1.x + v1.z * v1.z);
+    else
+        *v2 = V3(0, v1.z, -v1.y) / std::sqrt(v1.y * v1.y + v1.z * v1.z);
+    *v3 = Cross(v1, *v2);
+}
+static inline Float NextFloatUp(Float v) {
+    if (std::isinf(v) && v > 0.) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = bre_f2u(v);
+    if (v >= 0) ++ui;
+    else --ui;
+    return bre_u2f(ui);
+}
+static inline Float NextFloatDown(Float v) {
+    if (std::isinf(v) && v < 0.) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = bre_f2u(v);
+    if (v > 0) --ui;
+    else ++ui;
+    return bre_u2f(ui);
+}
+static inline V3 OffsetRayOrigin(const V3 &p, const V3 &pError, const V3 &n, const V3 &w) {
+    Float d = Dot(Abs(n), pError);
+    V3 offset = d * n;
+    if (Dot(w, n) < 0) offset = -offset;
+    V3 po = p + offset;
+    for (int i = 0; i < 3; ++i) {
+        if (offset[i] > 0) po[i] = NextFloatUp(po[i]);
+        else if (offset[i] < 0) po[i] = NextFloatDown(po[i]);
+    }
+    return po;
+}
+
+// ---- RGBSpectrum (spectrum.h) ----
+struct Spectrum {
+    Float c[3];
+    Spectrum(Float v = 0.f) { c[0] = c[1] = c[2] = v; }
+    Spectrum(Float a, Float b, Float d) {
+        c[0] = a;
+        c[1] = b;
+        c[2] = d;
+    }
+    explicit Spectrum(const float *p) : Spectrum(p[0], p[1], p[2]) {}
+    Spectrum operator*(const Spectrum &o) const { return Spectrum(c[0] * o.c[0], c[1] * o.c[1], c[2] * o.c[2]); }
+    Spectrum operator*(Float a) const { return Spectrum(c[0] * a, c[1] * a, c[2] * a); }
+    Spectrum operator/(Float a) const { return Spectrum(c[0] / a, c[1] / a, c[2] / a); }
+    Spectrum operator+(const Spectrum &o) const { return Spectrum(c[0] + o.c[0], c[1] + o.c[1], c[2] + o.c[2]); }
+    Spectrum operator-() const { return Spectrum(-c[0], -c[1], -c[2]); }
+    bool IsBlack() const { return c[0] == 0 && c[1] == 0 && c[2] == 0; }
+    Float y() const { return 0.212671f * c[0] + 0.715160f * c[1] + 0.072169f * c[2]; }
+};
+static inline Spectrum operator*(Float a, const Spectrum &s) { return s * a; }
+static inline Spectrum Exp(const Spectrum &s) {
+    return Spectrum(bre_expf(s.c[0]), bre_expf(s.c[1]), bre_expf(s.c[2]));
+}
+
+// ---- sampling (sampling.cpp:113-133, sampling.h:159-165) ----
+static inline void ConcentricSampleDisk(Float ux, Float uy, Float *dx, Float *dy) {
+    Float ox = 2.f * ux - 1, oy = 2.f * uy - 1;
+    if (ox == 0 && oy == 0) {
+        *dx = 0;
+        *dy = 0;
+        return;
+    }
+    Float theta, r;
+    if (std::fabs(ox) > std::fabs(oy)) {
+        r = ox;
+        theta = PiOver4 * (oy / ox);
+    } else {
+        r = oy;
+        theta = PiOver2 - PiOver4 * (ox / oy);
+    }
+    Float s, c;
+    bre_sincosf(theta, &s, &c);
+    *dx = c * r;
+    *dy = s * r;
+}
+static inline V3 CosineSampleHemisphere(Float ux, Float uy) {
+    Float dx, dy;
+    ConcentricSampleDisk(ux, uy, &dx, &dy);
+    Float z = std::sqrt(std::max((Float)0, 1 - dx * dx - dy * dy));
+    return V3(dx, dy, z);
+}
+
+// ---- Henyey-Greenstein (medium.cpp:194-218, medium.h:69-72) ----
+static inline Float PhaseHG(Float cosTheta, Float g) {
+    Float denom = 1 + g * g + 2 * g * cosTheta;
+    return Inv4Pi * (1 - g * g) / (denom * std::sqrt(denom));
+}
+static inline Float HG_Sample_p(Float g, const V3 &wo, V3 *wi, Float u0, Float u1) {
+    Float cosTheta;
+    if (std::abs(g) < 1e-3)
+        cosTheta = 1 - 2 * u0;
+    else {
+        Float sqrTerm = (1 - g * g) / (1 - g + 2 * g * u0);
+        cosTheta = (1 + g * g - sqrTerm * sqrTerm) / (2 * g);
+    }
+    Float sinTheta = std::sqrt(std::max((Float)0, 1 - cosTheta * cosTheta));
+    Float phi = 2 * Pi * u1;
+    V3 v1, v2;
+    CoordinateSystem(wo, &v1, &v2);
+    Float sp, cp;
+    bre_sincosf(phi, &sp, &cp);
+    *wi = sinTheta * cp * v1 + sinTheta * sp * v2 + cosTheta * (-wo);
+    return PhaseHG(-cosTheta, g);
+}
+static inline Float HG_p(Float g, const V3 &wo, const V3 &wi) { return PhaseHG(Dot(wo, wi), g); }
+
+// ---- rays, scene ----
+struct Ray {
+    V3 o, d;
+    Float tMax;
+    V3 operator()(Float t) const { return o + d * t; }
+};
+
+struct Quad {
+    V3 p0, e1, e2, n, ss, ts;
+    Float inv_e1sq, inv_e2sq, area;
+    Spectrum kd;
+};
+
+struct Scene {
+    std::vector<Quad> quads;
+    int light;
+    Spectrum Lemit;
+    bool medium;
+    Spectrum sigma_t, sigma_s;
+    Float g;
+};
+
+static Scene make_scene(const bre_scene *s) {
+    Scene sc;
+    for (int i = 0; i < s->n_quads; ++i) {
+        const bre_quad &q = s->quads[i];
+        Quad Q;
+        Q.p0 = V3(q.p0);
+        Q.e1 = V3(q.e1);
+        Q.e2 = V3(q.e2);
+        V3 c = Cross(Q.e1, Q.e2);
+        Q.area = c.Length();
+        Q.n = Normalize(c);
+        Q.ss = Normalize(Q.e1);
+        Q.ts = Cross(Q.n, Q.ss);
+        Q.inv_e1sq = 1 / Dot(Q.e1, Q.e1);
+        Q.inv_e2sq = 1 / Dot(Q.e2, Q.e2);
+        Q.kd = Spectrum(q.kd);
+        sc.quads.push_back(Q);
+    }
+    sc.light = s->light_quad;
+    sc.Lemit = Spectrum(s->light_L);
+    sc.medium = s->has_medium != 0;
+    Spectrum sa(s->sigma_a);
+    sc.sigma_s = Spectrum(s->sigma_s);
+    sc.sigma_t = sa + sc.sigma_s;
+    sc.g = s->g;
+    return sc;
+}
+
+struct Isect {
+    V3 p, pError, n;
+    int quad;
+};
+
+// Closest hit over all quads (strict <, so the lowest index wins a tie); sets ray.tMax like
+// GeometricPrimitive::Intersect (primitive.cpp:97-101).
+// One quad: plane solve, (u, v) in [0,1]^2, t in (0, ray.tMax); the hit point is rebuilt on the
+// quad with the parallelogram form of the triangle error bound.
+static bool IntersectQuad(const Quad &q, const Ray &ray, Float *tHit, Isect *isect) {
+    Float denom = Dot(q.n, ray.d);
+    if (denom == 0) return false;
+    Float t = Dot(q.n, q.p0 - ray.o) / denom;
+    if (!(t > 0 && t < ray.tMax)) return false;
+    V3 rel = ray(t) - q.p0;
+    Float u = Dot(rel, q.e1) * q.inv_e1sq;
+    Float v = Dot(rel, q.e2) * q.inv_e2sq;
+    if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) return false;
+    *tHit = t;
+    V3 ue1 = q.e1 * u, ve2 = q.e2 * v;
+    isect->p = q.p0 + ue1 + ve2;
+    isect->pError = (Abs(q.p0) + Abs(ue1) + Abs(ve2)) * gamma(6);
+    isect->n = q.n;
+    return true;
+}
+
+static bool Intersect(const Scene &sc, Ray &ray, Isect *isect) {
+    bool hit = false;
+    for (int i = 0; i < (int)sc.quads.size(); ++i) {
+        Float t;
+        Isect tmp;
+        if (!IntersectQuad(sc.quads[i], ray, &t, &tmp)) continue;
+        ray.tMax = t;
+        *isect = tmp;
+        isect->quad = i;
+        hit = true;
+    }
+    return hit;
+}
+
+// HomogeneousMedium (homogeneous.cpp:44-77)
+static Spectrum MediumTr(const Scene &sc, const Ray &ray) {
+    return Exp(-sc.sigma_t * std::min(ray.tMax * ray.d.Length(), MaxFloat));
+}
+// returns sampledMedium; *t = sampled distance.  (The returned weight is unused by the photon
+// tracer, which overwrites betaMedium with Tr, photonbeam.cpp:289.)
+static bool MediumSample(const Scene &sc, const Ray &ray, Sampler &sampler, Float *tOut) {
+    int channel = std::min((int)(sampler.Get1D() * 3), 3 - 1);
+    Float dist = -bre_logf(1 - sampler.Get1D()) / sc.sigma_t.c[channel];
+    Float t = std::min(dist * ray.d.Length(), ray.tMax);
+    *tOut = t;
+    return t < ray.tMax;
+}
+
+}  // namespace orp

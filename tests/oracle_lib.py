@@ -50,6 +50,14 @@ class Oracle:
         lib.ora_homogeneous_tr.argtypes = [P, P, I64, P, P, P]
         lib.ora_cosine_hemisphere.argtypes = [I64, P, P]
         lib.ora_fmath.argtypes = [I32, I64, P, P]
+        lib.ora_camera_pass.argtypes = [P, I32, I32, I32, I32, I32, I32, I64, P, P, P, P, P, P, P]
+        lib.ora_camera_pass.restype = I64
+        lib.ora_halton.argtypes = [I32, I32, I64, P, P, P, P, P]
+        lib.ora_radical_inverse.argtypes = [I32, U64]
+        lib.ora_radical_inverse.restype = F
+        lib.ora_scrambled_radical_inverse.argtypes = [I32, U64, P]
+        lib.ora_scrambled_radical_inverse.restype = F
+        lib.ora_shuffle.argtypes = [U64, I32, P]
 
     # -- primitives --
     def slab_pad(self) -> float:
@@ -133,6 +141,41 @@ class Oracle:
         self.lib.ora_fmath({"log": 0, "exp": 1, "sin": 2, "cos": 3}[kind], x.shape[0], _p(x), _p(y))
         return y
 
+    # -- camera pass (oracle/bre_oracle_camera.cpp) --
+    def camera_pass(self, scene, width, height, iteration=0, max_depth=5, render_surfaces=True, render_media=True):
+        """Segments in row-major pixel order (depth order within a pixel) + surface radiance (W*H, 3)."""
+        sp = ctypes.addressof(scene)
+        args = (sp, width, height, iteration, max_depth, int(render_surfaces), int(render_media))
+        n = int(self.lib.ora_camera_pass(*args, 0, None, None, None, None, None, None, None))
+        assert n >= 0, "camera path ran out of Halton dimensions"
+        out = {"o": np.zeros((n, 3), np.float32), "p": np.zeros((n, 3), np.float32), "d": np.zeros((n, 3), np.float32),
+               "tmax": np.zeros(n, np.float32), "pixel": np.zeros(n, np.int32), "depth": np.zeros(n, np.int32)}
+        ld = np.zeros((width * height, 3), np.float32)
+        n2 = self.lib.ora_camera_pass(*args, n, _p(out["o"]), _p(out["p"]), _p(out["d"]), _p(out["tmax"]),
+                                      _p(out["pixel"]), _p(out["depth"]), _p(ld))
+        assert n2 == n
+        out["surface"] = ld
+        return out
+
+    def halton(self, width, height, px, py, num, dim):
+        px, py, dim = (np.ascontiguousarray(x, np.int32) for x in (px, py, dim))
+        num = np.ascontiguousarray(num, np.int64)
+        out = np.zeros(px.shape[0], np.float32)
+        self.lib.ora_halton(width, height, px.shape[0], _p(px), _p(py), _p(num), _p(dim), _p(out))
+        return out
+
+    def radical_inverse(self, base_index, a):
+        return np.float32(self.lib.ora_radical_inverse(base_index, a))
+
+    def scrambled_radical_inverse(self, base_index, a, perm):
+        perm = np.ascontiguousarray(perm, np.uint16)
+        return np.float32(self.lib.ora_scrambled_radical_inverse(base_index, a, _p(perm)))
+
+    def shuffle(self, seq, perm):
+        perm = np.array(perm, np.uint16)
+        self.lib.ora_shuffle(seq, perm.shape[0], _p(perm))
+        return perm
+
     # -- gather through the reference SAH tree --
     def build(self, beams, sqrt_mode=0):
         return OracleBVH(self, beams, sqrt_mode)
@@ -200,7 +243,8 @@ _ORACLE = None
 def load_oracle() -> Oracle:
     global _ORACLE
     if _ORACLE is None:
-        srcs = [os.path.join(ORACLE_DIR, f) for f in ("bre_oracle.cpp", "bre_oracle_photon.cpp")]
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("bre_oracle.cpp", "bre_oracle_photon.cpp",
+                                                      "bre_oracle_camera.cpp", "ora_pbrt.h")]
         srcs += [os.path.join(ROOT, "include", f) for f in ("bre_fmath.h", "bre_scene.h")]
         if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(os.path.getmtime(f) for f in srcs):
             subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)

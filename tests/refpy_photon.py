@@ -431,3 +431,88 @@ def trace_photons(scene_struct, n_photons, iteration=0, max_depth=5, radius=0.01
 
 
 del math
+
+
+# ---- HaltonSampler restated (src/samplers/halton.cpp:63-127, lowdiscrepancy.cpp) ----
+class DefaultRNG(RNG):
+    """RNG() with PCG32_DEFAULT_STATE / PCG32_DEFAULT_STREAM (rng.h:145)."""
+
+    def __init__(self):
+        self.state = 0x853C49E6748FEA9B
+        self.inc = 0xDA3E39CB94B95BDB
+
+
+def uniform_u32_bounded(rng, b):
+    threshold = ((~b + 1) & 0xFFFFFFFF) % b
+    while True:
+        r = rng.u32()
+        if r >= threshold:
+            return r % b
+
+
+def shuffle(perm, rng):
+    n = len(perm)
+    for i in range(n):
+        other = i + uniform_u32_bounded(rng, n - i)
+        perm[i], perm[other] = perm[other], perm[i]
+    return perm
+
+
+def primes(n):
+    out = []
+    c = 2
+    while len(out) < n:
+        if all(c % q for q in out if q * q <= c):
+            out.append(c)
+        c += 1
+    return out
+
+
+class Halton:
+    def __init__(self, width, height, ndims=16):
+        self.primes = primes(ndims)
+        rng = DefaultRNG()
+        self.perms = [shuffle(list(range(p)), rng) for p in self.primes]
+        self.scales, self.exps = [], []
+        for res, base in ((width, 2), (height, 3)):
+            scale, e = 1, 0
+            while scale < min(res, 128):
+                scale *= base
+                e += 1
+            self.scales.append(scale)
+            self.exps.append(e)
+        self.stride = self.scales[0] * self.scales[1]
+        self.minv = [pow(self.scales[1], -1, self.scales[0]) if self.scales[0] > 1 else 0,
+                     pow(self.scales[0], -1, self.scales[1]) if self.scales[1] > 1 else 0]
+
+    def index(self, px, py, num):
+        off = 0
+        if self.stride > 1:
+            for i, (p, base) in enumerate(((px % 128, 2), (py % 128, 3))):
+                digits, inv = 0, p
+                for _ in range(self.exps[i]):
+                    digits = digits * base + inv % base
+                    inv //= base
+                off += digits * (self.stride // self.scales[i]) * self.minv[i]
+            off %= self.stride
+        return off + num * self.stride
+
+    def sample(self, index, dim):
+        if dim == 0:
+            a = index >> self.exps[0]
+            rev = int("{:064b}".format(a)[::-1], 2)
+            return f32(rev * 2.0 ** -64)
+        base = self.primes[dim]
+        perm = self.perms[dim] if dim >= 2 else list(range(base))
+        a = index if dim >= 2 else index // self.scales[1]
+        inv_base = f32(f32(1) / f32(base))
+        rev, inv_n = 0, f32(1)
+        while a:
+            rev = rev * base + perm[a % base]
+            inv_n = f32(inv_n * inv_base)
+            a //= base
+        if dim == 1:
+            v = f32(f32(rev) * inv_n)
+        else:
+            v = f32(inv_n * f32(f32(rev) + f32(f32(inv_base * f32(perm[0])) / f32(f32(1) - inv_base))))
+        return v if v < ONE_MINUS_EPS else ONE_MINUS_EPS
