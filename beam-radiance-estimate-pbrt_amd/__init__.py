@@ -23,6 +23,7 @@ BRE_OK = 0
 STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE_ERR_OOM",
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
+OPT_SHARD_RANK, OPT_SHARD_COUNT = 8, 9
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -169,6 +170,11 @@ class BeamGather:
 
     def set_option(self, opt: int, value: int):
         self._check(self.lib.bre_set_option(self.h, opt, int(value)))
+
+    def set_shard(self, rank: int, count: int):
+        """Camera pass walks only the 16x16 image tiles t with t % count == rank."""
+        self.set_option(OPT_SHARD_COUNT, int(count))
+        self.set_option(OPT_SHARD_RANK, int(rank))
 
     def set_stream(self, stream_handle: int | None):
         self._check(self.lib.bre_set_stream(self.h, stream_handle))

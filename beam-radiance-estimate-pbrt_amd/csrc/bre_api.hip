@@ -59,6 +59,7 @@ struct bre_ctx {
     int debug_mode = 0;
     int stack_limit = 0;
     int occupancy = 0;
+    int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
@@ -364,6 +365,16 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->split = (int)value;
         return BRE_OK;
     case BRE_OPT_PREFILTER: c->prefilter = value != 0; return BRE_OK;
+    case BRE_OPT_SHARD_RANK:
+        if (value < 0 || value >= c->shard_count)
+            return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_RANK must be in [0, shard count)");
+        c->shard_rank = (int)value;
+        return BRE_OK;
+    case BRE_OPT_SHARD_COUNT:
+        if (value < 1 || value > 65536) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_COUNT must be in 1..65536");
+        c->shard_count = (int)value;
+        if (c->shard_rank >= c->shard_count) c->shard_rank = 0;
+        return BRE_OK;
     case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
     case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
     case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 3 register budget
@@ -580,7 +591,7 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->cam_dev.as<DevCamera>(), c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
-                            c->cam_flags.as<unsigned int>(), c->stream));
+                            c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count, c->stream));
     // total = offs[S-1] + valid[S-1]
     HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
     int64_t last_off = 0;

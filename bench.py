@@ -1,23 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: beam-radiance estimates/sec at 1M photons (BASELINE.json metric), MI355X.
 
-Workload (config C2 of BASELINE.json, synthetic-fog of SURVEY.md §8d): 1,000,000 photon beams
-(radius 0.01, length ~ Exp(0.25) in the unit cube, PCG32 seed 12345) and one camera segment per
-pixel of a 512x512 image per GPU (seed 777); R_cur = 0.01.  One *step* is one iteration of the
-hot path with inputs already resident in HBM: the GPU BVH build over the iteration's beams
-(replacing PhotonBeamBVH's ctor) + the gather over every camera segment (photonbeam.cpp:494-508)
-accumulating into the framebuffer; with N>1 ranks, + one RCCL reduce of the framebuffer to rank 0.
-One *estimate* = the full gather for one segment.  value = all ranks' segments * steps / max-rank
-wall time of the timed steps.
+Default workload `c2` = BASELINE.json configs[1] / SURVEY.md §8d C2: the Cornell box in homogeneous
+fog (sigma_a 0.05, sigma_s 0.5, g 0), 512x512 film, 1,000,000 photons per iteration, maxdepth 5,
+initialbeamradius 0.01, alpha 0.5, 16 iterations (16 spp).  One *step* is one full iteration of
+PhotonBeamIntegrator::Render (photonbeam.cpp:362-562) on the GPU, everything resident in HBM:
+photon pass (emission + TracePhotonBeamRecursive, ~2.7M beams) + BVH build + camera pass + the
+gather of every camera segment into the pixels' Ld.  One *estimate* = the full gather for one
+camera segment (photonbeam.cpp:494-508).  value = segments gathered by all ranks / max-rank wall
+time of the timed steps.  Iteration k of the timed loop is the reference's iteration k (radius
+schedule and sampler indices included), so `--steps 16` is exactly the C2 render.
 
-Multi-GPU (weak scaling): the image is 512 x (512*N); its 16x16 tiles are dealt round-robin to the
-N ranks (photonbeam.cpp:345-347 tiles); the beams are replicated (every rank regenerates them from
-the same seeds) and each rank builds its own BVH; the framebuffer partial sums are reduced to rank 0.
+`--workload synthetic` = SURVEY.md §8d synthetic-fog kernel-only set (1M beams, seed 12345; one
+camera segment per pixel, seed 777): a step is BVH build + gather.
+
+Multi-GPU (weak scaling): the film is 512 x (512*N); its 16x16 tiles (photonbeam.cpp:345-347) are
+dealt round-robin to the N ranks; every rank traces the same photons (per-photon PCG32 sequences,
+so no communication) and builds its own BVH; the framebuffer partial sums are reduced to rank 0
+once per written image (the last step), one RCCL reduce.
 
 Also reported: `roofline` (SURVEY.md §8d algorithmic bytes of the gather kernel vs HBM peak; the
-kernel's average duration is measured with HIP events on the stream it is launched on) and
-`cpu_baseline` (the oracle's CPU restatement of the reference algorithm — SAH tree, per-query
-vector<shared_ptr>, all host threads — timed on a bounded sample of the same segments; rank 0, N=1).
+gather kernel's average duration measured with HIP events on the stream it is launched on;
+`traffic` = PMC FETCH_SIZE+WRITE_SIZE per launch from the committed rocprofv3 summary of the same
+workload, when present) and `cpu_baseline` (the oracle's CPU restatement of the reference
+algorithm — SAH tree, per-query vector<shared_ptr>, all host threads — timed on a bounded sample
+of the same segments and beams; rank 0, N=1).
 """
 from __future__ import annotations
 
@@ -40,12 +47,16 @@ VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=16, help="timed iterations (c2: 16 = the whole 16-spp render)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--beams", type=int, default=1_000_000)
+    ap.add_argument("--workload", choices=["c2", "synthetic"], default="c2")
+    ap.add_argument("--photons", type=int, default=1_000_000, help="c2: photons per iteration")
+    ap.add_argument("--beams", type=int, default=1_000_000, help="synthetic: beams")
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--height", type=int, default=512)
-    ap.add_argument("--radius", type=float, default=0.01)
+    ap.add_argument("--radius", type=float, default=0.01, help="initialbeamradius (c2) / R (synthetic)")
+    ap.add_argument("--alpha", type=float, default=0.5)
+    ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=1)
     ap.add_argument("--split", type=int, default=16, help="BVH subtrees per segment packet (kernels 1/3)")
@@ -55,9 +66,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
-                    help="camera: C2 primary segments (default, the metric); bounce: incoherent segments")
+                    help="synthetic: camera primary segments or incoherent bounce segments")
+    ap.add_argument("--profile-summary", default=None,
+                    help="rocprofv3 PMC summary (profiles/*/profile_summary.json) for roofline.traffic")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
+
+
+KERNEL_NAMES = {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
+                2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over"}
 
 
 def main():
@@ -66,7 +83,6 @@ def main():
     import torch.distributed as dist
 
     bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
-    synth = importlib.import_module("beam-radiance-estimate-pbrt_amd.synth")
     dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -81,19 +97,6 @@ def main():
 
     W, H = args.width, args.height * world
     frame = dmod.ShardedFrame(W, H, rank, world, device=dev)
-    npix = frame.npix
-    pixels = frame.pixels
-    beams = synth.fog_beams(args.beams, seed=12345, radius=args.radius)
-    if args.segment_kind == "camera":
-        segs = synth.camera_segments(W, H, seed=777, pixels=pixels)
-    else:  # incoherent secondary segments, one per owned pixel
-        segs = synth.bounce_segments(len(pixels), seed=778 + rank)
-        segs["pixel"] = pixels.astype(np.int32)
-    nseg = int(segs["tmax"].shape[0])
-    dB = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in beams.items()}
-    dS = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in segs.items()}
-    accum = frame.accum
-
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
     if args.debug_mode:
@@ -105,19 +108,14 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     g.set_stream(stream.cuda_stream)
-    R = args.radius
 
-    def step(ev=None):
-        g.set_beams_device(dB["start"], dB["end"], dB["radius"], dB["power"])
-        if ev is not None:
-            ev[0].record(stream)
-        g.gather_device(dS["o"], dS["p"], dS["d"], dS["tmax"], dS["pixel"], R, npix, accum=accum)
-        if ev is not None:
-            ev[1].record(stream)
-        frame.reduce_to_root(0)  # one RCCL reduce per written image (no-op at N=1)
+    if args.workload == "c2":
+        wl = C2Workload(args, bre, g, frame, rank, world)
+    else:
+        wl = SyntheticWorkload(args, bre, g, frame, rank, world, dev)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        wl.step(k, None, scratch=True)
     torch.cuda.synchronize(dev)
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -125,8 +123,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    nseg_local = 0
     for k in range(args.steps):
-        step(events[k])
+        nseg_local += wl.step(k, events[k], scratch=False)
+        if k == args.steps - 1:
+            frame.reduce_to_root(0)  # one RCCL reduce per written image (no-op at N=1)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -137,26 +138,21 @@ def main():
         tt = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, gather_ms = float(tt[0]), float(tt[1])
-        tot = torch.tensor([nseg], dtype=torch.int64, device=dev)
+        tot = torch.tensor([nseg_local], dtype=torch.int64, device=dev)
         dist.all_reduce(tot)
         total_seg = int(tot.item())
     else:
-        total_seg = nseg
+        total_seg = nseg_local
+    value = total_seg / elapsed
 
-    # untimed: counters and build time (HIP events inside libbre, same stream)
+    # untimed: one more step with counters and per-phase HIP-event timing inside libbre
     g.set_option(bre.OPT_COUNTERS, 1)
     g.set_option(bre.OPT_TIMING, 1)
-    g.set_beams_device(dB["start"], dB["end"], dB["radius"], dB["power"])
-    tmp = torch.zeros_like(accum)
-    g.gather_device(dS["o"], dS["p"], dS["d"], dS["tmax"], dS["pixel"], R, npix, accum=tmp)
-    g.synchronize()
+    diag = wl.diagnostics()
     st = g.stats()
-    g.close()
-
-    value = total_seg * args.steps / elapsed
-    c_mean = st["candidates"] / max(nseg, 1)
-    contrib_mean = st["contributions"] / max(nseg, 1)
-    waves = (nseg + 63) // 64
+    nseg_d = max(st["n_segments"], 1)
+    waves = (nseg_d + 63) // 64
+    c_mean = st["candidates"] / nseg_d
 
     result = {
         "metric": "beam-radiance estimates/sec at 1M photons",
@@ -170,55 +166,46 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (synthetic-fog: PCG32 seeds 12345 beams / 777 segments)",
-        "config": {
-            "workload": "C2 synthetic-fog: 1M-photon beam set, 512x512 camera segments per GPU, R=0.01",
-            "beams": args.beams,
-            "segments_per_gpu": nseg,
-            "image": [W, H],
-            "parallelism": f"image-tiles x{world}, beams replicated",
-            "kernel": {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
-                       2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over"}[args.kernel],
-            "leaf_size": args.leaf_size,
-            "split": args.split,
-            "prefilter": bool(args.prefilter),
-        },
+        "data": wl.data,
+        "config": wl.config(),
+        "estimates_per_step_per_gpu": nseg_local / args.steps,
         "gather_kernel_ms": gather_ms,
-        "bvh_build_ms": st["build_ms"],
         "candidates_per_estimate": c_mean,
-        "contributions_per_estimate": contrib_mean,
+        "contributions_per_estimate": st["contributions"] / nseg_d,
         "candidate_pair_tests_per_s": c_mean * value,
-        "node_visits_per_wave": st["node_visits"] / max(waves, 1),
-        "leaf_visits_per_wave": st["leaf_visits"] / max(waves, 1),
-        "beam_evals_per_wave": st["beam_evals"] / max(waves, 1),
-        "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / max(waves, 1),
-        "useful_beam_evals_per_wave": st["useful_beam_evals"] / max(waves, 1),
+        "node_visits_per_wave": st["node_visits"] / waves,
+        "leaf_visits_per_wave": st["leaf_visits"] / waves,
+        "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / waves,
         "max_stack_depth": st["max_stack_depth"],
         "redo_items": st["redo_items"],
-        "prefilter_rejects_per_estimate": st["prefilter_rejects"] / max(nseg, 1),
+        "prefilter_rejects_per_estimate": st["prefilter_rejects"] / nseg_d,
     }
+    result.update(diag)
 
-    cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(beams, segs, R, args.cpu_seconds)
+        cpu = cpu_baseline(wl.cpu_beams(), wl.cpu_segments(), wl.cpu_radius(), args.cpu_seconds, wl.name)
         result["cpu_baseline"] = cpu["report"]
-        # SURVEY §8d algorithmic bytes per estimate: 32 + 12 + 32*V + 40*C, V and C from the
+        # SURVEY.md §8d algorithmic bytes per estimate: 32 + 12 + 32*V + 40*C, V and C from the
         # reference SAH tree (oracle) on the CPU sample
         v_ref, c_ref = cpu["visit_mean"], cpu["cand_mean"]
         bytes_per_est = 32 + 12 + 32 * v_ref + 40 * c_ref
-        achieved = bytes_per_est * nseg / (gather_ms * 1e-3) / 1e9
+        per_launch = bytes_per_est * wl.segments_per_gather()
+        achieved = per_launch / (gather_ms * 1e-3) / 1e9
         result["roofline"] = {
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": None,
+            "traffic": pmc_traffic(args.profile_summary or wl.default_profile()),
+            "algorithmic_bytes_per_launch": per_launch,
             "bytes_per_estimate": bytes_per_est,
             "V_ref_tree": v_ref,
             "C": c_ref,
+            "kernel": "gather (k_gather_proxy + hand-over)",
         }
         result["speedup_vs_cpu"] = value / cpu["report"]["value"]
+    g.close()
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
@@ -229,7 +216,167 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(beams, segs, R, target_s):
+def pmc_traffic(path):
+    """HBM bytes per gather launch from a committed rocprofv3 PMC summary (FETCH_SIZE with the
+    gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md), or None when absent."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        summ = json.load(f)
+    tot = 0.0
+    calls = 0
+    for name, v in summ.items():
+        if name.startswith("k_gather"):
+            if "hbm_read_bytes_corrected" not in v:
+                continue
+            tot += (v["hbm_read_bytes_corrected"] + v.get("hbm_write_bytes", 0.0)) * v["calls"]
+            if name.startswith("k_gather_proxy"):
+                calls += v["calls"]
+    return tot / calls if calls else None
+
+
+class C2Workload:
+    """BASELINE.json configs[1]: Cornell box + homogeneous fog, 1M photons/iteration, 512x512."""
+
+    name = "c2"
+
+    def __init__(self, args, bre, g, frame, rank, world):
+        import torch
+
+        sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
+        self.args, self.bre, self.g, self.frame = args, bre, g, frame
+        self.scene = sc.cornell_scene(0.05, 0.5, 0.0)
+        self.W, self.H = frame.w, frame.h
+        g.set_shard(rank, world)
+        self.ld = frame.accum
+        self.scratch = torch.zeros_like(self.ld)
+        self.world = world
+        self.data = ("synthetic scene (SURVEY.md §8d C2: built-in Cornell box + homogeneous fog; photons and camera "
+                     "paths traced on the GPU)")
+        self.last_nseg = 0
+
+    def radius(self, it):
+        return self.bre.beam_radius_at(self.args.radius, self.args.alpha, it)
+
+    def step(self, it, ev, scratch):
+        a, g = self.args, self.g
+        ld = self.scratch if scratch else self.ld
+        R = self.radius(it)
+        self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
+        n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
+        if ev is not None:
+            ev[0].record()
+        g.gather_camera(R, ld)
+        if ev is not None:
+            ev[1].record()
+        self.last_nseg = n
+        return n
+
+    def diagnostics(self):
+        import torch
+
+        it = 0
+        self.step(it, None, scratch=True)
+        self.g.synchronize()
+        torch.cuda.synchronize()
+        st = self.g.stats()
+        self.R0 = self.radius(it)
+        return {"beams_per_iteration": st["n_beams"], "photon_pass_ms": st["photon_ms"], "bvh_build_ms": st["build_ms"],
+                "camera_pass_ms": st["camera_ms"], "gather_ms_iter0": st["gather_ms"]}
+
+    def segments_per_gather(self):
+        return self.last_nseg
+
+    def cpu_beams(self):
+        self.g.trace_photons(self.scene, self.args.photons, 0, self.args.max_depth, self.radius(0))
+        return self.g.get_beams()
+
+    def cpu_segments(self):
+        self.g.camera_pass(self.scene, self.W, self.H, 0, self.args.max_depth, True, True)
+        s = self.g.get_segments()
+        return {k: s[k] for k in ("o", "p", "d", "tmax", "pixel")}
+
+    def cpu_radius(self):
+        return self.radius(0)
+
+    def default_profile(self):
+        return os.path.join(ROOT, "profiles", "r03", "c2", "profile_summary.json")
+
+    def config(self):
+        a = self.args
+        return {"workload": "C2: Cornell box + homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0), 1M photons/iteration, "
+                            f"{a.width}x{a.height} per GPU, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
+                "photons_per_iteration": a.photons, "image": [self.W, self.H], "iterations_timed": a.steps,
+                "parallelism": f"image-tiles x{self.world}, photons traced on every rank",
+                "kernel": KERNEL_NAMES[a.kernel], "leaf_size": a.leaf_size, "split": a.split,
+                "prefilter": bool(a.prefilter)}
+
+
+class SyntheticWorkload:
+    """SURVEY.md §8d synthetic-fog: fixed beam set + one camera segment per pixel (kernel only)."""
+
+    name = "synthetic"
+
+    def __init__(self, args, bre, g, frame, rank, world, dev):
+        import torch
+
+        synth = importlib.import_module("beam-radiance-estimate-pbrt_amd.synth")
+        self.args, self.g, self.frame, self.world = args, g, frame, world
+        self.beams = synth.fog_beams(args.beams, seed=12345, radius=args.radius)
+        pixels = frame.pixels
+        if args.segment_kind == "camera":
+            self.segs = synth.camera_segments(frame.w, frame.h, seed=777, pixels=pixels)
+        else:  # incoherent secondary segments, one per owned pixel
+            self.segs = synth.bounce_segments(len(pixels), seed=778 + rank)
+            self.segs["pixel"] = pixels.astype(np.int32)
+        self.nseg = int(self.segs["tmax"].shape[0])
+        self.dB = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in self.beams.items()}
+        self.dS = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in self.segs.items()}
+        self.scratch = torch.zeros_like(frame.accum)
+        self.data = "synthetic (synthetic-fog: PCG32 seeds 12345 beams / 777 segments)"
+
+    def step(self, it, ev, scratch):
+        g, dB, dS = self.g, self.dB, self.dS
+        acc = self.scratch if scratch else self.frame.accum
+        g.set_beams_device(dB["start"], dB["end"], dB["radius"], dB["power"])
+        if ev is not None:
+            ev[0].record()
+        g.gather_device(dS["o"], dS["p"], dS["d"], dS["tmax"], dS["pixel"], self.args.radius, self.frame.npix,
+                        accum=acc)
+        if ev is not None:
+            ev[1].record()
+        return self.nseg
+
+    def diagnostics(self):
+        self.step(0, None, scratch=True)
+        self.g.synchronize()
+        st = self.g.stats()
+        return {"bvh_build_ms": st["build_ms"], "beams": st["n_beams"]}
+
+    def segments_per_gather(self):
+        return self.nseg
+
+    def cpu_beams(self):
+        return self.beams
+
+    def cpu_segments(self):
+        return self.segs
+
+    def cpu_radius(self):
+        return self.args.radius
+
+    def default_profile(self):
+        return os.path.join(ROOT, "profiles", "r02", "profile_summary.json")
+
+    def config(self):
+        a = self.args
+        return {"workload": "C2 synthetic-fog: 1M-photon beam set, 512x512 camera segments per GPU, R=0.01",
+                "beams": a.beams, "segments_per_gpu": self.nseg, "image": [self.frame.w, self.frame.h],
+                "parallelism": f"image-tiles x{self.world}, beams replicated", "kernel": KERNEL_NAMES[a.kernel],
+                "leaf_size": a.leaf_size, "split": a.split, "prefilter": bool(a.prefilter)}
+
+
+def cpu_baseline(beams, segs, R, target_s, name):
     """Oracle = CPU restatement of the reference algorithm (not pbrt itself: the reference build was
     denied).  SAH build single-threaded (as photonbeambvh.cpp:232), gather on all
     available host threads over 256-segment chunks pulled dynamically (ParallelFor2D-like)."""
@@ -260,14 +407,15 @@ def cpu_baseline(beams, segs, R, target_s):
     out = bvh.gather(sample, R, nthreads=threads, chunk=max(1, min(256, m // (4 * threads) or 1)))
     gather_s = time.perf_counter() - t
     bvh.close()
+    nb = beams["radius"].shape[0]
     return {
         "report": {
             "value": m / gather_s,
             "unit": "estimates/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"{m} random camera segments of the same 512x512 workload, {gather_s:.1f} s gather on "
-                      f"{threads} threads; SAH build of {beams['radius'].shape[0]} beams took {build_s:.1f} s "
+            "sample": f"{m} random camera segments of the {name} workload (iteration 0), gather {gather_s:.1f} s on "
+                      f"{threads} threads against all {nb} beams; SAH build of the {nb} beams took {build_s:.1f} s "
                       f"(1 thread, not in value)",
             "sah_build_s": build_s,
         },

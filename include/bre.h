@@ -69,8 +69,13 @@ typedef enum bre_option {
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
     BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 16) */
-    BRE_OPT_PREFILTER = 7    /* kernels 1/3: 0/1 conservative line-distance reject before the exact
+    BRE_OPT_PREFILTER = 7,   /* kernels 1/3: 0/1 conservative line-distance reject before the exact
                                 closest-point code (default 1; results are identical either way) */
+    BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles t (the reference's
+                                camera-pass tiles, photonbeam.cpp:345-347) with t % count == rank */
+    BRE_OPT_SHARD_COUNT = 9  /* camera pass: number of image-tile shards (default 1 = all tiles).
+                                Set the count before the rank.  Per-pixel results do not depend on
+                                the sharding, so summing the shards' Ld gives the 1-shard image. */
 } bre_option;
 
 typedef struct bre_stats {

@@ -149,3 +149,31 @@ def test_render_matches_iterations(bre, oracle, scene_mod, torch):
     assert img.shape == (h, w, 3)
     assert _rel_l2(img.reshape(-1, 3), ref) <= 1e-3
     del R
+
+
+def test_camera_pass_tile_shards_partition_the_film(bre, scene_mod, torch):
+    """BRE_OPT_SHARD_*: the shards' segment sets are a disjoint cover of the 1-shard set (bit-exact
+    per (pixel, depth)), each shard keeps only its own 16x16 tiles, and the surface terms add up."""
+    s = scene_mod.cornell_scene()
+    w, h, world = 72, 40, 3
+    full = _camera(bre, torch, s, w, h, iteration=3, max_depth=5)
+    parts = []
+    surf = np.zeros_like(full["surface"])
+    for r in range(world):
+        with bre.BeamGather(0) as g:
+            g.set_shard(r, world)
+            sf = torch.zeros((w * h, 3), dtype=torch.float32, device="cuda")
+            g.camera_pass(s, w, h, iteration=3, max_depth=5, surface=sf)
+            seg = g.get_segments()
+        torch.cuda.synchronize()
+        pix = seg["pixel"]
+        tile = (pix // w // 16) * ((w + 15) // 16) + (pix % w) // 16
+        assert np.all(tile % world == r)
+        parts.append(seg)
+        surf += sf.cpu().numpy()
+    merged = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    _assert_segments_equal(merged, full)
+    assert np.array_equal(surf.view(np.uint32), full["surface"].view(np.uint32))
+    with bre.BeamGather(0) as g:
+        with pytest.raises(bre.BreError):
+            g.set_shard(3, 3)
