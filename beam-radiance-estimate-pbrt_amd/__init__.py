@@ -23,7 +23,7 @@ BRE_OK = 0
 STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE_ERR_OOM",
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
-OPT_SHARD_RANK, OPT_SHARD_COUNT = 8, 9
+OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [

@@ -61,6 +61,10 @@ struct bre_ctx {
     int occupancy = 0;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
+    int leaf2 = 32;          // auto mode: leaf size of the tile tree kernel 4 takes hand-overs on
+    int built_leaf2 = 0;     // 0: no tile tree for the current beam set
+    int roots2_split = -1;
+    DevMem nodes2, roots2;
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     int built_leaf_size = 1;
@@ -116,6 +120,8 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = 0;
     c->nnodes = 0;
     c->roots_split = -1;
+    c->roots2_split = -1;
+    c->built_leaf2 = 0;
     c->stats = bre_stats{};
     c->stats.n_beams = n;
     if (n == 0) return BRE_OK;
@@ -177,6 +183,19 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.visit = c->visit.as<unsigned int>();
     HIPCHK(c, launch_pack(b, nvalid, c->stream));
     HIPCHK(c, launch_hierarchy(b, nvalid, c->stream));
+    // auto mode: a second hierarchy over the same sorted beam records with leaf tiles of leaf2
+    // beams, for the packets kernel 3 hands over to kernel 4 (leaf_parent / visit are reused:
+    // the second tree has fewer leaves, and stream order serialises the two builds)
+    if (c->kernel == 0 && K <= kProxyMaxLeafHost && c->leaf2 > K) {
+        const int K2 = c->leaf2;
+        const int64_t nleaf2 = (nvalid + K2 - 1) / K2;
+        HIPCHK(c, c->nodes2.ensure((size_t)(nleaf2 > 1 ? nleaf2 - 1 : 1) * sizeof(Node)));
+        BuildBuffers b2 = b;
+        b2.leaf_size = K2;
+        b2.nodes = c->nodes2.as<Node>();
+        HIPCHK(c, launch_hierarchy(b2, nvalid, c->stream));
+        c->built_leaf2 = K2;
+    }
     if (c->timing) {
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventSynchronize(c->ev[1]));
@@ -229,6 +248,9 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.partial = nullptr;
     a.pcnt = nullptr;
     a.redo = nullptr;
+    a.nodes2 = nullptr;
+    a.roots2 = nullptr;
+    a.leaf2 = c->built_leaf2;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
@@ -237,8 +259,10 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     }
     // auto (0): the packet-proxy kernel 3 (with kernel 1 as its device-side overflow fallback)
     // when leaf clusters are small enough for its candidate list, else kernel 1
+    // auto (0): kernel 3 on the small-leaf tree with kernel 4 on the tile tree taking the packets it
+    // hands over; with leaf clusters too large for kernel 3, kernel 4 alone
     int kernel = c->kernel;
-    if (kernel == 0) kernel = c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 1;
+    if (kernel == 0 && c->built_leaf2 == 0) kernel = c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 4;
     if (kernel == 3 && c->built_leaf_size > kProxyMaxLeafHost)
         return fail(c, BRE_ERR_STATE, "kernel 3 needs BRE_OPT_LEAF_SIZE <= %d", kProxyMaxLeafHost);
     if (kernel != 2) {
@@ -250,6 +274,15 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         a.roots = c->roots.as<int32_t>();
         a.partial = c->partial.as<float>();
+        if (kernel == 0) {
+            HIPCHK(c, c->roots2.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
+            if (c->roots2_split != c->split) {
+                HIPCHK(c, launch_roots(c->nodes2.as<Node>(), c->split, c->roots2.as<int32_t>(), c->stream));
+                c->roots2_split = c->split;
+            }
+            a.nodes2 = c->nodes2.as<Node>();
+            a.roots2 = c->roots2.as<int32_t>();
+        }
         HIPCHK(c, c->redo.ensure((size_t)(nseg + 63) / 64 + 16));
         a.redo = c->redo.as<uint8_t>();
         if (c->counters) {
@@ -348,11 +381,11 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
     case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
     case BRE_OPT_KERNEL:
-        if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..3");
+        if (value < 0 || value > 4) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..4");
         c->kernel = (int)value;
         return BRE_OK;
     case BRE_OPT_LEAF_SIZE:
-        if (value < 1 || value > 16) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_LEAF_SIZE must be in 1..16");
+        if (value < 1 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_LEAF_SIZE must be in 1..64");
         c->leaf_size = (int)value;
         return BRE_OK;
     case BRE_OPT_SQRT_MODE:
@@ -365,6 +398,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->split = (int)value;
         return BRE_OK;
     case BRE_OPT_PREFILTER: c->prefilter = value != 0; return BRE_OK;
+    case BRE_OPT_TILE_LEAF:
+        if (value < 1 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_TILE_LEAF must be in 1..64");
+        c->leaf2 = (int)value;
+        return BRE_OK;
     case BRE_OPT_SHARD_RANK:
         if (value < 0 || value >= c->shard_count)
             return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_RANK must be in [0, shard count)");

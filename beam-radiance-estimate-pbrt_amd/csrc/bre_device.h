@@ -107,7 +107,11 @@ struct GatherArgs {
     int debug_mode;        // 0 normal; 1 timing-only: traversal without leaf evaluation
     int stack_limit;       // kernel 3 LDS stack entries to use (0 = all); tests force the fallback
     int occupancy;         // kernel 3 register budget: min waves per SIMD (1, 6 or 8)
-    uint8_t *redo;         // kernel 3: [packets] flags of packets handed to kernel 1
+    uint8_t *redo;         // kernel 3: [packets] flags of packets handed to kernel 1 (or 4)
+    // auto mode (kernel 0): the tile tree over the same beam records for kernel 4's hand-over
+    const Node *nodes2;
+    const int32_t *roots2;
+    int leaf2;
 };
 
 // gather kernels (bre_gather.hip)

@@ -132,6 +132,25 @@ __device__ __forceinline__ bool far_from_lines(const Lane &L, const BeamV &r, fl
     return (tn - 1e-6f * tl) > (maxd * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
 }
 
+// far_from_lines with FMAs and the hardware sqrt: the same bound, evaluated to within a few ulps
+// of the exact values, far inside its margins (1e-6 relative on |t.n|, |n| and the 1e-5 eps).
+// Any rejection is still a proof that the reference's computed distance is >= maxd.
+__device__ __forceinline__ bool far_from_lines_fast(f3 o, f3 au, float mag_a, float omax, f3 b0, f3 bu, float maxd) {
+    if (mag_a == 0.0f) return false;
+    const f3 t = sub3(b0, o);
+    const f3 n = mk(__builtin_fmaf(au.y, bu.z, -(au.z * bu.y)), __builtin_fmaf(au.z, bu.x, -(au.x * bu.z)),
+                    __builtin_fmaf(au.x, bu.y, -(au.y * bu.x)));
+    const float nn = __builtin_fmaf(n.x, n.x, __builtin_fmaf(n.y, n.y, n.z * n.z));
+    if (!(nn >= 1e-2f)) return false;
+    const float tn = fabsf(__builtin_fmaf(t.x, n.x, __builtin_fmaf(t.y, n.y, t.z * n.z)));
+    const float tl = fabsf(t.x) + fabsf(t.y) + fabsf(t.z);
+    const float bmax = fmaxf(fmaxf(fabsf(b0.x), fabsf(b0.y)), fabsf(b0.z));
+    const float mag = omax + bmax + 10.0f * tl;
+    const float eps = 1e-5f * mag + 1e-6f;
+    const float nl = __builtin_amdgcn_sqrtf(nn) * 1.000001f;  // v_sqrt_f32 (1 ulp) rounded up
+    return (tn - 1e-6f * tl) > (maxd * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
+}
+
 // Evaluate one beam record for one lane: reference box test, closest points, kernel.
 struct Prof {
     unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0;
@@ -359,7 +378,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
     const int w = threadIdx.x >> 6;
     const int64_t s = grp * kWaveBlock + threadIdx.x;
     // behind kernel 3, only the packets it handed over (incoherent, or out of LDS stack) run here
-    if (redo && (s >= nseg || !redo[s >> 6])) return;  // per wave: all lanes share the packet
+    if (redo) {  // per wave (one packet): a ragged last packet keeps all its lanes
+        const int64_t pk = (grp * kWaveBlock + (int64_t)w * 64) >> 6;
+        if (pk * 64 >= nseg || !redo[pk]) return;
+    }
     Lane L;
     const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
     float cr = 0.f, cg = 0.f, cb = 0.f;
@@ -710,6 +732,301 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Kernel 4 (k_gather_tile): wave-packet traversal over leaf TILES of up to 64 beams with two
+// levels of wavefront compaction of the per-pair work.
+//
+// At dense candidate sets (the C2 Cornell fog: a camera segment passes ~16% of all beam boxes,
+// and packets of incoherent bounce segments share few of them) the exact per-pair code executed
+// under a 64-lane mask is the cost: a wave runs ComputeClosestPoints whenever ANY lane needs it,
+// with ~3% of the lanes active.  Here:
+//   1. a hit leaf tile's beam boxes are staged in LDS by one vector load per lane, and the tile is
+//      scanned beam by beam with only the reference's box test per lane (~25 VALU ops, box read
+//      by an LDS broadcast);
+//   2. (segment lane, beam) pairs that pass are appended to a per-wave LDS queue (ballot +
+//      mbcnt); every 64 queued pairs run the conservative distance prefilter with all lanes busy
+//      (each lane takes one pair, its segment from LDS and the beam line from L2);
+//   3. the prefilter's survivors go to a second queue; every 64 of those run
+//      ComputeClosestPoints and the kernel, again one pair per lane, and add the contribution to
+//      the segment's LDS accumulator.
+// Same per-pair arithmetic as kernel 1; only the float summation order of a segment's
+// contributions differs (deterministic: queue order is fixed by the traversal).
+constexpr int kTileBlock = 256;  // 4 waves
+constexpr int kQueueCap = 128;   // >= 63 left over + 64 appended by one beam / one flush
+constexpr int kTileMax = 32;     // beams staged in LDS at a time (longer leaves go in chunks)
+
+struct TileShared {
+    float4 tile[kTileMax][4];  // staged BeamRec lines of the current leaf chunk
+    float acc[3][64];          // per-segment RGB accumulators
+    int32_t cnt[64];           // per-segment contribution counts (counters only)
+    uint16_t q0[kQueueCap];    // box-hit queue: tile slot | segment lane << 8
+    int32_t qb1[kQueueCap];    // prefilter-survivor queue: beam index
+    uint8_t ql1[kQueueCap];    //                           segment lane
+    int32_t stk[kStackDepth];
+};
+
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+__device__ __forceinline__ float lane_f(float v, int src) { return __shfl(v, src); }
+
+// Stage 3: exact closest points + kernel for n queued pairs (one per lane; all lanes call).
+template <bool COUNT>
+__device__ __forceinline__ void tile_exact(TileShared &sh, const Lane &M, int first, int n,
+                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
+                                           Prof &pf) {
+    const int lane = threadIdx.x & 63;
+    const bool on = lane < n;
+    const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
+    const int32_t b = sh.qb1[e];
+    const int sl = sh.ql1[e];
+    // the pair's segment, from its owner lane's registers
+    const f3 o = mk(lane_f(M.o.x, sl), lane_f(M.o.y, sl), lane_f(M.o.z, sl));
+    const f3 p = mk(lane_f(M.p.x, sl), lane_f(M.p.y, sl), lane_f(M.p.z, sl));
+    const f3 au = mk(lane_f(M.au.x, sl), lane_f(M.au.y, sl), lane_f(M.au.z, sl));
+    const float mag_a = lane_f(M.mag_a, sl);
+    const BeamV r = load_beam(recs, b);
+    if (COUNT && lane == 0) ++pf.ccp_waves;
+    if (on) {
+        const float maxd = R + r.radius;  // MaxDistance = currentBeamRadius + beam->radius
+        float dist;
+        const bool ok = closest_distance(o, p, au, mag_a, r.b0, r.bu, r.mag_b, dist);
+        if (ok & (dist < maxd)) {
+            const float rr = dist / maxd;
+            const float w = sqrtf(1.0f - rr * rr);
+            const float4 pv = pw[b];
+            atomicAdd(&sh.acc[0][sl], pv.x * w);
+            atomicAdd(&sh.acc[1][sl], pv.y * w);
+            atomicAdd(&sh.acc[2][sl], pv.z * w);
+            if (COUNT) atomicAdd(&sh.cnt[sl], 1);
+        }
+    }
+}
+
+// Stage 2: prefilter n box-hit pairs of the staged tile (one per lane; all lanes call); the
+// survivors are appended to queue 1, which is drained in batches of 64.  Without the prefilter,
+// every pair is forwarded.
+template <bool COUNT, bool PREF>
+__device__ __forceinline__ void tile_filter(TileShared &sh, const Lane &M, int first, int n, int64_t tile0, int &h1, int &t1,
+                                            const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
+                                            Prof &pf) {
+    const int lane = threadIdx.x & 63;
+    const bool on = lane < n;
+    const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
+    const unsigned qv = sh.q0[e];
+    const int j = (int)(qv & 0xffu), sl = (int)(qv >> 8);
+    bool need = on;
+    if (PREF) {
+        const f3 o = mk(lane_f(M.o.x, sl), lane_f(M.o.y, sl), lane_f(M.o.z, sl));
+        const f3 au = mk(lane_f(M.au.x, sl), lane_f(M.au.y, sl), lane_f(M.au.z, sl));
+        const float mag_a = lane_f(M.mag_a, sl);
+        const float omax = lane_f(M.omax, sl);
+        const float4 y = sh.tile[j][1], z = sh.tile[j][2], wv = sh.tile[j][3];
+        need = on && !far_from_lines_fast(o, au, mag_a, omax, mk(y.z, y.w, z.x), mk(z.y, z.z, z.w), R + wv.y);
+        if (COUNT) pf.rejects += on & !need;
+    }
+    const unsigned long long m = __ballot(need);
+    if (m == 0ull) return;
+    if (need) {
+        const int pos = (t1 + lanes_below(m)) & (kQueueCap - 1);
+        sh.qb1[pos] = (int32_t)(tile0 + j);
+        sh.ql1[pos] = (uint8_t)sl;
+    }
+    t1 += __popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (t1 - h1 >= 64) {
+        // FIFO: survivors are evaluated in queue order, so a segment's contributions are summed
+        // in the same order with or without the prefilter (bit-identical results)
+        tile_exact<COUNT>(sh, M, h1, 64, recs, pw, R, pf);
+        h1 += 64;
+        if (h1 >= 1024) {
+            h1 -= 1024;
+            t1 -= 1024;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <bool COUNT, bool PREF, int MINW>
+__global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
+    int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
+    const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
+    const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
+    int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int dbg,
+    const uint8_t *__restrict__ redo) {
+    __shared__ TileShared shm[kTileBlock / 64];
+    int sub;
+    int64_t grp;
+    if (S >= 8) {
+        const unsigned per = (unsigned)S >> 3;
+        const unsigned q = blockIdx.x >> 3;
+        sub = (int)((blockIdx.x & 7u) * per + q % per);
+        grp = q / per;
+    } else {
+        sub = (int)(blockIdx.x % (unsigned)S);
+        grp = blockIdx.x / (unsigned)S;
+    }
+    if (sub >= roots[S]) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    TileShared &sh = shm[w];
+    const int64_t s = grp * kTileBlock + threadIdx.x;
+    // behind kernel 3 (auto), only the packets it handed over run here; the test is per wave (one
+    // packet), so a ragged last packet keeps all 64 lanes (tile staging and shuffles need them)
+    if (redo) {
+        const int64_t pk = (grp * kTileBlock + (int64_t)w * 64) >> 6;
+        if (pk * 64 >= nseg || !redo[pk]) return;
+    }
+    Lane L;
+    const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
+    sh.acc[0][lane] = 0.f;
+    sh.acc[1][lane] = 0.f;
+    sh.acc[2][lane] = 0.f;
+    sh.cnt[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const bool any_inf = __ballot(L.has_inf) != 0ull;  // some lane has an axis-parallel direction
+    int cand = 0;
+    unsigned long long visits = 0;
+    Prof pf;
+    int h0 = 0, t0 = 0, h1 = 0, t1 = 0;  // wave-uniform FIFO ring heads / tails
+
+    // scan one leaf: its beam lines are staged in LDS kTileMax at a time; per lane the reference
+    // box test, hits queued; full batches, and each chunk's remainder, go through the filter
+    const auto leaf = [&](int32_t c, bool lane_on) {
+        const int64_t first = (int64_t)(~c) * leaf_size;
+        const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+        if (COUNT) {
+            ++pf.leaves;
+            pf.beams += cnt;
+        }
+        if (dbg == 1) return;  // timing-only: traversal without leaf work
+        for (int base = 0; base < cnt; base += kTileMax) {
+            const int nb = min(kTileMax, cnt - base);
+            const int64_t tile0 = first + base;
+            __builtin_amdgcn_wave_barrier();
+            {
+                // 64 lanes copy nb lines of 4 x 16 B: lane -> (beam lane >> 1, half lane & 1)
+                const int bj = lane >> 1, h = (lane & 1) * 2;
+                if (bj < nb) {
+                    const float4 *q = reinterpret_cast<const float4 *>(recs + tile0 + bj);
+                    const float4 u = q[h], v = q[h + 1];
+                    sh.tile[bj][h] = u;
+                    sh.tile[bj][h + 1] = v;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int j = 0; j < nb; ++j) {
+                const float4 x = sh.tile[j][0], y = sh.tile[j][1];
+                const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+                float te;
+                bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
+                if (any_inf) {
+                    if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
+                }
+                if (COUNT) cand += hit;
+                const unsigned long long m = __ballot(hit);
+                if (m == 0ull) continue;
+                if (COUNT) ++pf.useful;
+                if (hit) sh.q0[(t0 + lanes_below(m)) & (kQueueCap - 1)] = (uint16_t)(j | (lane << 8));
+                t0 += __popcll(m);
+                if (t0 - h0 >= 64) {
+                    __builtin_amdgcn_wave_barrier();
+                    if (dbg != 2) tile_filter<COUNT, PREF>(sh, L, h0, 64, tile0, h1, t1, recs, pw, R, pf);
+                    h0 += 64;
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (t0 > h0) {
+                __builtin_amdgcn_wave_barrier();
+                if (dbg != 2) tile_filter<COUNT, PREF>(sh, L, h0, t0 - h0, tile0, h1, t1, recs, pw, R, pf);
+            }
+            h0 = t0 = 0;  // the chunk's queue is drained (its entries index this chunk's tile)
+        }
+    };
+
+    if (__ballot(valid) != 0ull) {
+        const int32_t root = roots[sub];
+        if (root < 0) {
+            leaf(root, valid);
+        } else {
+            int node = root;
+            int sp = 0;
+            while (true) {
+                node = __builtin_amdgcn_readfirstlane(node);
+                const NodeV n = load_node(nodes, node);
+                if (COUNT) ++visits;
+                const int32_t c0 = n.c0, c1 = n.c1;
+                float te0 = 0.f, te1 = 0.f;
+                const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, L.o, L.invs, L.tmax, te0);
+                const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, L.o, L.invs, L.tmax, te1);
+                const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+                bool go0 = m0 != 0ull, go1 = m1 != 0ull;
+                if (go0 && c0 < 0) {
+                    leaf(c0, h0);
+                    go0 = false;
+                }
+                if (go1 && c1 < 0) {
+                    leaf(c1, h1);
+                    go1 = false;
+                }
+                if (go0 && go1) {
+                    const unsigned long long both = m0 & m1;
+                    bool first0 = true;
+                    if (both != 0ull) {
+                        const int fl = __ffsll((long long)both) - 1;
+                        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
+                        const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
+                        first0 = !(b < a);
+                    }
+                    const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
+                    if (sp >= kStackDepth) {
+                        if (lane == 0) atomicOr(&ctr->flags, 1u);
+                        break;
+                    }
+                    sh.stk[sp] = far;
+                    ++sp;
+                    node = near;
+                } else if (go0) {
+                    node = c0;
+                } else if (go1) {
+                    node = c1;
+                } else {
+                    if (sp == 0) break;
+                    --sp;
+                    node = sh.stk[sp];
+                }
+            }
+        }
+        // drain the prefilter survivors
+        __builtin_amdgcn_wave_barrier();
+        if (dbg != 2 && t1 > h1) tile_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
+        h1 = t1 = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+        float *dst = partial + 3 * ((int64_t)sub * nseg + s);
+        dst[0] = sh.acc[0][lane];
+        dst[1] = sh.acc[1][lane];
+        dst[2] = sh.acc[2][lane];
+        if (COUNT) {
+            pcnt[2 * ((int64_t)sub * nseg + s)] = cand;
+            pcnt[2 * ((int64_t)sub * nseg + s) + 1] = sh.cnt[lane];
+        }
+    }
+    if (COUNT) {
+        unsigned long long rj = pf.rejects;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) rj += __shfl_xor(rj, off);
+        if (lane == 0) {
+            atomicAdd(&ctr->node_visits, visits);
+            atomicAdd(&ctr->leaf_visits, pf.leaves);
+            atomicAdd(&ctr->beam_evals, pf.beams);
+            atomicAdd(&ctr->useful_beam_evals, pf.useful);
+            atomicAdd(&ctr->prefilter_rejects, rj);
+            atomicAdd(&ctr->ccp_wave_evals, pf.ccp_waves);
+        }
+    }
+}
+
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the
 // segment's sum to its pixel (one float atomic per channel, PhotonBeamPixel::Ld +=).  With
 // counters, also sum the per-subtree candidate / contribution counts.
@@ -717,10 +1034,12 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
                                                 const int32_t *__restrict__ pcnt, const int32_t *__restrict__ roots,
                                                 int S, const int32_t *__restrict__ pixel, int64_t npix,
                                                 float *__restrict__ accum, float *__restrict__ seg_rgb,
-                                                int32_t *__restrict__ seg_counts, DevCounters *ctr) {
+                                                int32_t *__restrict__ seg_counts, DevCounters *ctr,
+                                                const uint8_t *__restrict__ redo, const int32_t *__restrict__ roots2) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool in = s < nseg;
-    const int nr = roots[S];
+    // packets handed over to the second tree (auto mode) hold that tree's subtree partials
+    const int nr = (redo && in && redo[s >> 6]) ? roots2[S] : roots[S];
     float cr = 0.f, cg = 0.f, cb = 0.f;
     long long c = 0, k = 0;
     if (in) {
@@ -900,7 +1219,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
                                a.nvalid, a.leaf_size, a.ctr);
         return hipGetLastError();
     }
-    if (kernel == 3) {
+    if (kernel == 3 || kernel == 0) {
         const int64_t packets = (a.nseg + 63) / 64;
         hipError_t em = hipMemsetAsync(a.redo, 0, (size_t)packets, s);
         if (em != hipSuccess) return em;
@@ -923,6 +1242,42 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         hipError_t e3 = hipGetLastError();
         if (e3 != hipSuccess) return e3;
     }
+    if (kernel == 4 || kernel == 0) {
+        // kernel 0 (auto): kernel 3 above on the small-leaf tree, then kernel 4 on the tile tree
+        // for the packets kernel 3 handed over (incoherent, or out of LDS stack)
+        const bool ho = kernel == 0;
+        const Node *nodes4 = ho ? a.nodes2 : a.nodes;
+        const int32_t *roots4 = ho ? a.roots2 : a.roots;
+        const int leaf4 = ho ? a.leaf2 : a.leaf_size;
+        const uint8_t *redo4 = ho ? a.redo : nullptr;
+        const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
+#define BRE_LAUNCH_TILE_W(C, P, W)                                                                                \
+    hipLaunchKernelGGL((k_gather_tile<C, P, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R, \
+                       a.partial, a.pcnt, a.recs, a.pow, nodes4, a.nvalid, leaf4, roots4, a.split,                   \
+                       a.ctr, a.debug_mode, redo4)
+#define BRE_LAUNCH_TILE(C, P)                      \
+    do {                                           \
+        if (a.occupancy >= 8)                      \
+            BRE_LAUNCH_TILE_W(C, P, 8);            \
+        else                                       \
+            BRE_LAUNCH_TILE_W(C, P, 1);            \
+    } while (0)
+        if (counters) {
+            if (a.prefilter) BRE_LAUNCH_TILE(true, true);
+            else BRE_LAUNCH_TILE(true, false);
+        } else {
+            if (a.prefilter) BRE_LAUNCH_TILE(false, true);
+            else BRE_LAUNCH_TILE(false, false);
+        }
+#undef BRE_LAUNCH_TILE
+#undef BRE_LAUNCH_TILE_W
+        hipError_t e4 = hipGetLastError();
+        if (e4 != hipSuccess) return e4;
+        hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial,
+                           counters ? a.pcnt : nullptr, a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb,
+                           counters ? a.seg_counts : nullptr, a.ctr, redo4, a.roots2);
+        return hipGetLastError();
+    }
     const int64_t groups = (a.nseg + kWaveBlock - 1) / kWaveBlock;
     const dim3 grid((unsigned int)(groups * a.split));
     const uint8_t *redo = kernel == 3 ? a.redo : nullptr;  // kernel 1 as kernel 3's device-side fallback
@@ -942,7 +1297,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial,
                        counters ? a.pcnt : nullptr, a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb,
-                       counters ? a.seg_counts : nullptr, a.ctr);
+                       counters ? a.seg_counts : nullptr, a.ctr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
                     help="synthetic: camera primary segments or incoherent bounce segments")
     ap.add_argument("--profile-summary", default=None,
@@ -74,7 +75,8 @@ def parse():
 
 
 KERNEL_NAMES = {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
-                2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over"}
+                2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over",
+                4: "leaf tiles + wavefront-compacted pair queue"}
 
 
 def main():
@@ -146,9 +148,12 @@ def main():
     value = total_seg / elapsed
 
     # untimed: one more step with counters and per-phase HIP-event timing inside libbre
-    g.set_option(bre.OPT_COUNTERS, 1)
-    g.set_option(bre.OPT_TIMING, 1)
-    diag = wl.diagnostics()
+    if not args.no_diag:
+        g.set_option(bre.OPT_COUNTERS, 1)
+        g.set_option(bre.OPT_TIMING, 1)
+        diag = wl.diagnostics()
+    else:
+        diag = {}
     st = g.stats()
     nseg_d = max(st["n_segments"], 1)
     waves = (nseg_d + 63) // 64

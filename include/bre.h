@@ -63,19 +63,25 @@ typedef enum bre_status {
 typedef enum bre_option {
     BRE_OPT_COUNTERS = 1,    /* 0/1: per-segment candidate / contribution / node-visit counting */
     BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
-    BRE_OPT_KERNEL = 3,      /* 0 = auto (3 when leaf size <= 4, else 1), 1 = depth-first wave-packet
-                                traversal, 2 = thread-per-segment, 3 = packet-proxy traversal with
-                                incoherent / overflowing packets handed to kernel 1 on the device */
-    BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..16 (default 1); applies at next build */
+    BRE_OPT_KERNEL = 3,      /* 0 = auto: with leaf size <= 4, kernel 3 on that tree and kernel 4 on a
+                                second tree with BRE_OPT_TILE_LEAF-beam leaves (same beam records)
+                                for the packets kernel 3 hands over; larger leaves: kernel 4.
+                                1 = depth-first wave-packet traversal, 2 = thread-per-segment,
+                                3 = packet-proxy traversal with incoherent / overflowing packets
+                                handed to kernel 1 on the device, 4 = depth-first traversal over
+                                leaf tiles with wavefront-compacted pair queues */
+    BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..64 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
     BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 16) */
     BRE_OPT_PREFILTER = 7,   /* kernels 1/3: 0/1 conservative line-distance reject before the exact
                                 closest-point code (default 1; results are identical either way) */
     BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles t (the reference's
                                 camera-pass tiles, photonbeam.cpp:345-347) with t % count == rank */
-    BRE_OPT_SHARD_COUNT = 9  /* camera pass: number of image-tile shards (default 1 = all tiles).
+    BRE_OPT_SHARD_COUNT = 9, /* camera pass: number of image-tile shards (default 1 = all tiles).
                                 Set the count before the rank.  Per-pixel results do not depend on
                                 the sharding, so summing the shards' Ld gives the 1-shard image. */
+    BRE_OPT_TILE_LEAF = 10   /* auto mode: beams per leaf tile of the hand-over tree, 1..64 (default
+                                32); applies at the next build */
 } bre_option;
 
 typedef struct bre_stats {

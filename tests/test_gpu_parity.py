@@ -36,8 +36,8 @@ def ctxs(bre):
         c.close()
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
-@pytest.mark.parametrize("leaf", [1, 4, 8])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("leaf", [1, 4, 8, 64])
 def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     if kernel == 3 and leaf > 4:
         pytest.skip("kernel 3 needs leaf clusters <= 4 (tested in test_kernel3_rejects_large_leaves)")
@@ -56,13 +56,13 @@ def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     assert st["contributions"] == int(ref["contrib"].sum())
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
 def test_bounce_segments_match_oracle(bre, synth, oracle, kernel):
     beams = synth.fog_beams(3000, seed=99)
     segs = synth.bounce_segments(3000, seed=5)
     R = 0.013
     ref = oracle.build(beams).gather(segs, R)
-    with bre.BeamGather(0, counters=True, kernel=kernel) as g:
+    with bre.BeamGather(0, counters=True, kernel=kernel, leaf_size=32 if kernel == 4 else None) as g:
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
         out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, counts=True)
     assert np.array_equal(out["counts"][:, 0], ref["cand"])
@@ -224,7 +224,7 @@ def test_deterministic_per_segment(bre, synth):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel", [1, 3])
+@pytest.mark.parametrize("kernel", [0, 1, 3, 4])
 @pytest.mark.parametrize("split", [1, 2, 8, 64])
 def test_subtree_split_matches_oracle(bre, synth, oracle, split, kernel):
     beams = synth.fog_beams(4000, seed=51)
@@ -251,7 +251,7 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         segs = synth.camera_segments(64, 64, seed=64) if kind == "camera" else synth.bounce_segments(4096, seed=65)
         R = 0.01
     outs = []
-    for k, pf in ((1, False), (1, True), (3, False), (3, True)):
+    for k, pf in ((1, False), (1, True), (3, False), (3, True), (4, False), (4, True)):
         with bre.BeamGather(0, counters=True, kernel=k, prefilter=pf) as g:
             g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
             outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True))
@@ -262,6 +262,25 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         assert np.array_equal(outs[0]["counts"], o["counts"])
         assert _seg_close(o["seg_rgb"], outs[0]["seg_rgb"]) <= SEG_RTOL
     assert np.array_equal(outs[2]["seg_rgb"], outs[3]["seg_rgb"])
+    assert np.array_equal(outs[4]["seg_rgb"], outs[5]["seg_rgb"])
+
+
+@pytest.mark.parametrize("leaf", [16, 64])
+def test_kernel4_dense_incoherent_is_deterministic(bre, synth, oracle, leaf):
+    """Kernel 4's compaction queue and LDS accumulators on a dense, incoherent set (long beams,
+    large radius: many candidates per lane): exact sets, sums to rounding, bit-identical reruns."""
+    beams = synth.fog_beams(5000, seed=71, radius=0.03, mean_length=0.7)
+    segs = synth.bounce_segments(3000, seed=72)
+    ref = oracle.build(beams).gather(segs, 0.04)
+    runs = []
+    for _ in range(2):
+        with bre.BeamGather(0, counters=True, kernel=4, leaf_size=leaf) as g:
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            runs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.04, counts=True))
+    assert np.array_equal(runs[0]["counts"][:, 0], ref["cand"])
+    assert np.array_equal(runs[0]["counts"][:, 1], ref["contrib"])
+    assert _seg_close(runs[0]["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    assert np.array_equal(runs[0]["seg_rgb"], runs[1]["seg_rgb"])
 
 
 def test_kernel3_rejects_large_leaves(bre, synth):
@@ -286,3 +305,28 @@ def test_kernel3_stack_overflow_falls_back_exactly(bre, synth, oracle):
     assert np.array_equal(out["counts"][:, 0], ref["cand"])
     assert np.array_equal(out["counts"][:, 1], ref["contrib"])
     assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+
+@pytest.mark.parametrize("tile_leaf", [8, 32, 64])
+def test_auto_handover_mixed_packets(bre, synth, oracle, tile_leaf):
+    """Auto mode: coherent camera packets stay in kernel 3, incoherent bounce packets go to kernel 4
+    on the tile tree; one gather over both kinds matches the oracle exactly (sets) and to rounding."""
+    beams = synth.fog_beams(6000, seed=81, mean_length=0.4)
+    cam = synth.camera_segments(32, 32, seed=82)
+    bnc = synth.bounce_segments(2048, seed=83, npix=1024)
+    segs = {k: np.concatenate([cam[k], bnc[k]]) for k in cam}
+    R = 0.012
+    ref = oracle.build(beams).gather(segs, R, npix=1024)
+    accum = np.zeros((1024, 3), np.float32)
+    with bre.BeamGather(0, counters=True, kernel=0) as g:
+        g.set_option(bre.OPT_TILE_LEAF, tile_leaf)
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, npix=1024, accum=accum,
+                       counts=True)
+        st = g.stats()
+    assert st["redo_items"] > 0  # the bounce packets were handed over
+    assert np.array_equal(out["counts"][:, 0], ref["cand"])
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    assert _rel_l2(accum, ref["accum"]) <= 1e-6
