@@ -207,7 +207,7 @@ def main():
             "bytes_per_estimate": bytes_per_est,
             "V_ref_tree": v_ref,
             "C": c_ref,
-            "kernel": "gather (k_gather_proxy + hand-over)",
+            "kernel": "gather (k_gather_proxy + k_gather_tile hand-over)",
         }
         result["speedup_vs_cpu"] = value / cpu["report"]["value"]
     g.close()
@@ -305,7 +305,7 @@ class C2Workload:
         return self.radius(0)
 
     def default_profile(self):
-        return os.path.join(ROOT, "profiles", "r03", "c2", "profile_summary.json")
+        return os.path.join(ROOT, "profiles", "r04", "profile_summary.json")
 
     def config(self):
         a = self.args
