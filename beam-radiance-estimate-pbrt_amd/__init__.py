@@ -30,7 +30,7 @@ EXPORTS = [
     "bre_abi_version", "bre_create", "bre_destroy", "bre_last_error", "bre_set_option",
     "bre_set_stream", "bre_synchronize", "bre_get_stats", "bre_set_beams",
     "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
-    "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell",
+    "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell", "bre_scene_cornell_smoke", "bre_smoke_density",
     "bre_camera_pass", "bre_gather_camera", "bre_get_segments", "bre_render_iteration", "bre_render",
 ]
 
@@ -112,6 +112,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_get_beams.restype = I32
     lib.bre_scene_cornell.argtypes = [P, F, F, F]
     lib.bre_scene_cornell.restype = None
+    lib.bre_scene_cornell_smoke.argtypes = [P, F, F, F, I32, P]
+    lib.bre_scene_cornell_smoke.restype = None
+    lib.bre_smoke_density.argtypes = [I32, ctypes.c_uint64, P]
+    lib.bre_smoke_density.restype = None
     lib.bre_camera_pass.argtypes = [P, P, I32, I32, I32, I32, I32, I32, P, ctypes.POINTER(I64)]
     lib.bre_camera_pass.restype = I32
     lib.bre_gather_camera.argtypes = [P, F, P]

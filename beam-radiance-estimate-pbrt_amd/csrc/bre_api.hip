@@ -3,6 +3,8 @@
 // plus a message for bre_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -75,7 +77,7 @@ struct bre_ctx {
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem counters_buf, roots, partial, pcnt, redo;
     // photon pass
-    DevMem ph_scene, ph_counts, ph_offsets, ph_tmp;
+    DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // camera pass
     DevMem cam_dev, cam_perms, cs_o, cs_p, cs_d, cs_t, cs_pix, cs_valid, cam_offs, cam_tmp, cam_flags;
     DevMem seg_o, seg_p, seg_d, seg_t, seg_pix, seg_depth;
@@ -362,7 +364,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo,
-                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->cam_dev, &c->cam_perms,
+                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
                      &c->seg_depth};
@@ -488,6 +490,43 @@ bre_status bre_set_beams_device(bre_ctx *c, int64_t n, const float *start, const
     return build(c, n, start, end, radius, power);
 }
 
+// Medium parameters: GridDensityMedium needs a density grid with a positive maximum (the ctor's
+// invMaxDensity = 1/maxDensity, grid.h:73-76); a non-uniform sigma_t is accepted as pbrt does
+// (its Error() only reports it, grid.h:66-70) and channel 0 is used.
+static bre_status check_medium(bre_ctx *c, const bre_scene *scene, const char *fn) {
+    if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "%s: null scene", fn);
+    if (scene->has_medium < BRE_MEDIUM_NONE || scene->has_medium > BRE_MEDIUM_GRID)
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: unknown medium type %d", fn, scene->has_medium);
+    if (scene->has_medium != BRE_MEDIUM_GRID) return BRE_OK;
+    const int64_t nx = scene->grid_n[0], ny = scene->grid_n[1], nz = scene->grid_n[2];
+    if (nx < 1 || ny < 1 || nz < 1 || nx * ny * nz > BRE_MAX_GRID_CELLS)
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: grid dimensions must be >= 1 with at most %d cells", fn,
+                    BRE_MAX_GRID_CELLS);
+    if (!scene->grid_density) return fail(c, BRE_ERR_INVALID_ARG, "%s: null grid_density", fn);
+    if (!(grid_max_density(scene) > 0))
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: grid density maximum must be > 0", fn);
+    return BRE_OK;
+}
+
+// DevScene (+ the density grid of a GridDensityMedium) into ph_scene on the context's stream
+static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
+    const float *dd = nullptr;
+    if (scene->has_medium == BRE_MEDIUM_GRID) {
+        const size_t n = (size_t)scene->grid_n[0] * scene->grid_n[1] * scene->grid_n[2];
+        HIPCHK(c, c->grid_dens.ensure(n * sizeof(float)));
+        HIPCHK(c, hipMemcpyAsync(c->grid_dens.ptr, scene->grid_density, n * sizeof(float), hipMemcpyHostToDevice,
+                                 c->stream));
+        dd = c->grid_dens.as<float>();
+    }
+    DevScene hs;
+    prepare_scene(scene, &hs, dd);
+    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
+    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    // the host copies are read by the DMA before the call returns
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
+}
+
 bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photons, int32_t iteration,
                              int32_t max_depth, float beam_radius, int64_t *n_beams) {
     if (!c) return BRE_ERR_INVALID_ARG;
@@ -499,17 +538,17 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     if (scene->n_quads < 1 || scene->n_quads > BRE_MAX_QUADS || scene->light_quad < 0 ||
         scene->light_quad >= scene->n_quads)
         return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: bad quad count or light index");
-    bre_status st = set_device(c);
+    bre_status st = check_medium(c, scene, "bre_trace_photons");
     if (st != BRE_OK) return st;
-    DevScene hs;
-    prepare_scene(scene, &hs);
+    st = set_device(c);
+    if (st != BRE_OK) return st;
+    st = upload_scene(c, scene);
+    if (st != BRE_OK) return st;
     const size_t N = (size_t)n_photons;
-    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
     HIPCHK(c, c->ph_counts.ensure((N + 1) * sizeof(int32_t)));
     HIPCHK(c, c->ph_offsets.ensure((N + 1) * sizeof(int64_t)));
     const size_t tmp = count_scan_temp_bytes(n_photons);
     HIPCHK(c, c->ph_tmp.ensure(tmp + 16));
-    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
     const uint64_t seq0 = (uint64_t)iteration * (uint64_t)n_photons + 1;
     const DevScene *ds = c->ph_scene.as<DevScene>();
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
@@ -589,13 +628,13 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
         return fail(c, BRE_ERR_INVALID_ARG, "bre_camera_pass: bad film size or iteration");
     if (max_depth < 1 || max_depth > BRE_MAX_DEPTH)
         return fail(c, BRE_ERR_INVALID_ARG, "bre_camera_pass: max_depth must be in [1, %d]", BRE_MAX_DEPTH);
+    st = check_medium(c, scene, "bre_camera_pass");
+    if (st != BRE_OK) return st;
     st = set_device(c);
     if (st != BRE_OK) return st;
     // scene + camera/Halton tables (rebuilt when the scene or film changes)
-    DevScene hs;
-    prepare_scene(scene, &hs);
-    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
-    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    st = upload_scene(c, scene);
+    if (st != BRE_OK) return st;
     if (c->cam_w != width || c->cam_h != height || memcmp(&c->cam_scene, scene, sizeof(bre_scene)) != 0) {
         DevCamera cam;
         std::vector<uint16_t> perms;
@@ -640,7 +679,6 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&flags, c->cam_flags.ptr, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (flags & 1u) return fail(c, BRE_ERR_STATE, "bre_camera_pass: a path needed more than %d Halton dimensions", kHaltonDims);
     const int64_t n = last_off + last_valid;
     const size_t N = (size_t)(n > 0 ? n : 1);
     HIPCHK(c, c->seg_o.ensure(N * 3 * sizeof(float)));
@@ -790,6 +828,58 @@ void bre_scene_cornell(bre_scene *s, float sigma_a, float sigma_s, float g) {
     memcpy(s->cam_look, look, 12);
     memcpy(s->cam_up, up, 12);
     s->cam_fov_deg = 60.f;
+}
+
+void bre_scene_cornell_smoke(bre_scene *s, float sigma_a, float sigma_s, float g, int32_t n, const float *density) {
+    if (!s) return;
+    bre_scene_cornell(s, sigma_a, sigma_s, g);
+    s->has_medium = BRE_MEDIUM_GRID;
+    s->grid_n[0] = s->grid_n[1] = s->grid_n[2] = n;
+    memset(s->world_to_medium, 0, sizeof(s->world_to_medium));
+    for (int k = 0; k < 4; ++k) s->world_to_medium[5 * k] = 1.f;  // the grid spans the box's unit cube
+    s->grid_density = density;
+}
+
+void bre_smoke_density(int32_t n, uint64_t seed, float *density) {
+    if (!density || n < 1) return;
+    // 3 octaves of trilinear value noise on lattices of 5, 9, 17 points per axis, values from
+    // PCG32 sequence `seed` (rng.h:78-85) in lattice order
+    bre::Pcg r;
+    bre::pcg_seed(r, seed);
+    std::vector<float> lat[3];
+    int m[3];
+    for (int k = 0; k < 3; ++k) {
+        m[k] = (4 << k) + 1;
+        lat[k].resize((size_t)m[k] * m[k] * m[k]);
+        for (float &v : lat[k]) v = bre::pcg_float(r);
+    }
+    for (int z = 0; z < n; ++z)
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                const float p[3] = {(x + 0.5f) / n, (y + 0.5f) / n, (z + 0.5f) / n};
+                float v = 0.f, amp = 0.5f;
+                for (int k = 0; k < 3; ++k, amp *= 0.5f) {
+                    const int L = m[k] - 1;
+                    int i[3];
+                    float f[3];
+                    for (int a = 0; a < 3; ++a) {
+                        const float q = p[a] * L;
+                        i[a] = std::min((int)q, L - 1);
+                        f[a] = q - (float)i[a];
+                    }
+                    float acc = 0.f;
+                    for (int c = 0; c < 8; ++c) {
+                        const int dx = c & 1, dy = (c >> 1) & 1, dz = c >> 2;
+                        const float w = (dx ? f[0] : 1 - f[0]) * (dy ? f[1] : 1 - f[1]) * (dz ? f[2] : 1 - f[2]);
+                        acc += w * lat[k][((size_t)(i[2] + dz) * m[k] + (i[1] + dy)) * m[k] + (i[0] + dx)];
+                    }
+                    v += amp * acc;
+                }
+                const float dx = p[0] - 0.5f, dy = p[1] - 0.45f, dz = p[2] - 0.55f;
+                const float rr = std::sqrt(dx * dx + dy * dy + dz * dz);
+                const float shape = std::min(1.f, std::max(0.f, (0.45f - rr) / 0.2f));
+                density[((size_t)z * n + y) * n + x] = std::max(0.f, 2.f * v - 0.4f) * shape;
+            }
 }
 
 bre_status bre_gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d,

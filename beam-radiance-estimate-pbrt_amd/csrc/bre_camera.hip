@@ -189,12 +189,16 @@ __device__ __forceinline__ float scrambled_radical_inverse(uint32_t base, const 
 
 __device__ __forceinline__ uint32_t rev_bits32(uint32_t n) { return __builtin_bitreverse32(n); }
 
+// AwesomeSampler(0, tileSampler, 1000, GoodPixelIndex) (photonbeam.cpp:188-224, 459): draws
+// 1..1000 are HaltonSampler dimensions 0..999 of the pixel's sample index (the two advance in
+// lockstep until the switch; a Get2D that would cross it is drawn from the RNG whole), later draws
+// come from PCG32 sequence GoodPixelIndex, two-draw points built right to left as in g++.
 struct HaltonDev {
     const DevCamera *C;
     const uint16_t *perms;
     int64_t index;
-    int dim;
-    bool overflow;
+    int count;  // AwesomeSampler::sampleCount
+    Pcg rng;
     __device__ __forceinline__ float sample(int d) const {
         if (d == 0) {
             const uint64_t a = (uint64_t)(index >> C->base_exp[0]);
@@ -205,23 +209,32 @@ struct HaltonDev {
         return scrambled_radical_inverse((uint32_t)C->primes[d], perms + C->prime_sums[d], (uint64_t)index);
     }
     __device__ __forceinline__ float get1d() {
-        if (dim >= kHaltonDims) {
-            overflow = true;
-            return 0.f;
-        }
-        return sample(dim++);
+        ++count;
+        if (count <= kHaltonDims) return sample(count - 1);
+        return pcg_float(rng);
     }
     __device__ __forceinline__ void get2d(float &x, float &y) {
-        if (dim + 1 >= kHaltonDims) {
-            overflow = true;
-            x = y = 0.f;
-            return;
+        count += 2;
+        if (count <= kHaltonDims) {
+            x = sample(count - 2);
+            y = sample(count - 1);
+        } else {
+            pcg_2d(rng, x, y);
         }
-        x = sample(dim);
-        y = sample(dim + 1);
-        dim += 2;
     }
 };
+__device__ __forceinline__ float smp_1d(HaltonDev &h) { return h.get1d(); }
+
+// GoodPixelIndex = globalNumPixels (always 0) + iterNumPixels++ (photonbeam.cpp:351, 457-458).  The
+// reference increments that counter from every camera-pass thread without synchronisation, so its
+// value is scheduling-dependent; we use the single-threaded order (tiles row-major, ParallelFor2D's
+// serial loop, then Bounds2i iteration order x-fastest inside the 16x16 tile).  It only seeds the
+// PCG32 draws past the 1000th of a path.
+__device__ __forceinline__ uint64_t good_pixel_index(int W, int H, int px, int py) {
+    const int tx = px >> 4, ty = py >> 4;
+    const int th = min(16, H - ty * 16), tw = min(16, W - tx * 16);
+    return (uint64_t)ty * 16 * (uint64_t)W + (uint64_t)tx * 16 * (uint64_t)th + (uint64_t)((py & 15) * tw + (px & 15));
+}
 
 __device__ __forceinline__ uint64_t inv_radical_inverse(uint64_t base, uint64_t inverse, int ndig) {
     uint64_t idx = 0;
@@ -294,8 +307,8 @@ __device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {
 }
 
 // EstimateDirect for the scene's one area light (integrator.cpp:108-214), handleMedia = true
-__device__ void estimate_direct(const DevScene &S, f3 p, f3 perr, const PQuad &q, f3 wo, float usx, float usy,
-                                float ulx, float uly, float Ld[3]) {
+__device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr, const PQuad &q, f3 wo, float usx,
+                                float usy, float ulx, float uly, float Ld[3]) {
     const PQuad &L = S.q[S.light];
     Ld[0] = Ld[1] = Ld[2] = 0.f;
     float scat_pdf = 0.f;
@@ -338,7 +351,7 @@ __device__ void estimate_direct(const DevScene &S, f3 p, f3 perr, const PQuad &q
                 Li[0] = Li[1] = Li[2] = 0.f;  // every quad has a material
             } else if (S.medium) {
                 float tr[3];
-                medium_tr(S, rd, tmax, tr);
+                medium_tr_any(S, hs, ro, rd, tmax, tr);
                 for (int c = 0; c < 3; ++c) Li[c] = Li[c] * (1.f * tr[c]);
             }
             if (!black3(Li)) {
@@ -368,7 +381,7 @@ __device__ void estimate_direct(const DevScene &S, f3 p, f3 perr, const PQuad &q
             float tr[3] = {1.f, 1.f, 1.f};
             if (S.medium) {
                 float t2[3];
-                medium_tr(S, wi, tmax, t2);
+                medium_tr_any(S, hs, ro, wi, tmax, t2);
                 for (int c = 0; c < 3; ++c) tr[c] = tr[c] * t2[c];
             }
             if (found && h.quad == S.light && dot3(L.n, neg3(wi)) > 0 && !black3(S.Le))
@@ -398,7 +411,8 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
     if (shard_count > 1 && ((py >> 4) * ((C.width + 15) >> 4) + (px >> 4)) % shard_count != shard_rank) return;
     const int pixel = py * C.width + px;
 
-    HaltonDev hs{Cp, perms, halton_index(C, px, py, iteration), 0, false};
+    HaltonDev hs{Cp, perms, halton_index(C, px, py, iteration), 0, Pcg{}};
+    pcg_seed(hs.rng, good_pixel_index(C.width, C.height, px, py));
     float fx, fy, lx, ly;
     hs.get2d(fx, fy);
     fx = (float)px + fx;
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
         Hit hit;
         if (!intersect_scene(S, o, d, tmax, hit)) break;  // area lights: Le(ray) = 0
         float mb[3] = {1.f, 1.f, 1.f};
-        if (S.medium) medium_tr(S, d, tmax, mb);
+        if (S.medium) medium_tr_any(S, hs, o, d, tmax, mb);
         if (render_media) {
             const int64_t k = depth * nslots + slot;
             so[3 * k + 0] = o.x;
@@ -455,7 +469,7 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
         hs.get2d(ulx, uly);
         hs.get2d(usx, usy);
         float ed[3];
-        estimate_direct(S, hit.p, hit.perr, q, normalize3(wo), usx, usy, ulx, uly, ed);
+        estimate_direct(S, hs, hit.p, hit.perr, q, normalize3(wo), usx, usy, ulx, uly, ed);
         for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + beta[c] * (ed[c] / 1.0f);
         if (depth < max_depth - 1) {
             float ux, uy, pdf = 0.f, f[3];
@@ -474,7 +488,6 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
             for (int c = 0; c < 3; ++c) beta[c] = beta[c] / cp;
         }
     }
-    if (hs.overflow) atomicOr(flags, 1u);
     if (surface && render_surfaces)
         for (int c = 0; c < 3; ++c) surface[3 * pixel + c] += Ld[c];
 }

@@ -17,16 +17,33 @@
 
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
+
 #include "bre_device.h"
 #include "bre_trace.h"
 
 namespace bre {
 
-void prepare_scene(const bre_scene *s, DevScene *out) {
+float grid_max_density(const bre_scene *s) {
+    float mx = 0;
+    const int64_t n = (int64_t)s->grid_n[0] * s->grid_n[1] * s->grid_n[2];
+    for (int64_t i = 0; i < n; ++i) mx = std::max(mx, s->grid_density[i]);
+    return mx;
+}
+
+void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
     DevScene d{};
     d.n_quads = s->n_quads;
     d.light = s->light_quad;
-    d.medium = s->has_medium ? 1 : 0;
+    d.medium = s->has_medium == BRE_MEDIUM_GRID ? BRE_MEDIUM_GRID : (s->has_medium ? BRE_MEDIUM_HOMOGENEOUS : 0);
+    if (d.medium == BRE_MEDIUM_GRID) {
+        // GridDensityMedium ctor (grid.h:58-77): sigma_t = (sigma_a + sigma_s)[0]; invMaxDensity
+        for (int k = 0; k < 3; ++k) d.gn[k] = s->grid_n[k];
+        d.grid_sigma_t = s->sigma_a[0] + s->sigma_s[0];
+        d.grid_inv_max = 1 / grid_max_density(s);
+        for (int k = 0; k < 16; ++k) d.w2m[k] = s->world_to_medium[k];
+        d.density = d_density;
+    }
     for (int c = 0; c < 3; ++c) {
         d.Le[c] = s->light_L[c];
         d.sigma_t[c] = s->sigma_a[c] + s->sigma_s[c];  // HomogeneousMedium ctor: sigma_a + sigma_s
@@ -122,7 +139,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
             } else {
                 bool scattered = false;
                 float ts = 0;
-                if (S.medium) scattered = medium_sample(S, rng, d, tmax, ts);
+                if (S.medium) scattered = medium_sample_any(S, rng, o, d, tmax, ts);
                 if (black3(beta)) {
                     stop = true;
                 } else if (scattered) {
@@ -132,7 +149,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
                     pcg_2d(rng, hx, hy);
                     const f3 wi = hg_sample(S.g, neg3(d), hx, hy);
                     float tr[3];
-                    medium_tr(S, d, tmax, tr);
+                    medium_tr_any(S, rng, o, d, tmax, tr);
                     Frame &f = stk[sp++];
                     f.o = o;
                     f.d = d;
@@ -156,7 +173,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
             resume = false;
             // beam for the whole surface-hit segment, powerEnd = Tr * beta (:289-294)
             float bm[3] = {1.f, 1.f, 1.f};
-            if (S.medium) medium_tr(S, d, tmax, bm);
+            if (S.medium) medium_tr_any(S, rng, o, d, tmax, bm);
             if (EMIT) {
                 const int64_t k = w + cnt;
                 bs[3 * k + 0] = o.x;

@@ -151,15 +151,23 @@ struct PQuad {
 };
 
 struct DevScene {
-    int n_quads, light, medium, pad;
+    int n_quads, light, medium, pad;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
     float Le[3];
     float sigma_t[3];
     float g;
     PQuad q[BRE_MAX_QUADS];
+    // GridDensityMedium (grid.h:50-80): sigma_t = (sigma_a + sigma_s)[0], invMaxDensity
+    int gn[3];
+    float grid_sigma_t, grid_inv_max;
+    float w2m[16];            // WorldToMedium, row-major
+    const float *density;     // device copy of the grid (nx*ny*nz)
 };
 
-// host: derive per-quad constants exactly as oracle/ora_pbrt.h make_scene does
-void prepare_scene(const bre_scene *s, DevScene *out);
+// host: derive per-quad constants exactly as oracle/ora_pbrt.h make_scene does; `d_density` is
+// the device copy of s->grid_density (grid media only)
+void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density = nullptr);
+// host: GridDensityMedium ctor's maxDensity loop (grid.h:73-76), std::max order
+float grid_max_density(const bre_scene *s);
 
 struct Hit {
     f3 p, perr;
@@ -199,6 +207,10 @@ __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, f
     return hit;
 }
 
+// Sampler draws: the photon pass draws from PCG32 (AwesomeHaltonSampler past its 1000 Halton
+// dimensions); the camera pass overloads smp_1d for its AwesomeSampler (bre_camera.hip).
+__device__ __forceinline__ float smp_1d(Pcg &r) { return pcg_float(r); }
+
 // HomogeneousMedium::Tr, homogeneous.cpp:44-48
 __device__ __forceinline__ void medium_tr(const DevScene &S, f3 d, float tmax, float tr[3]) {
     const float x = smin(tmax * len3(d), kMaxFloat);
@@ -206,20 +218,159 @@ __device__ __forceinline__ void medium_tr(const DevScene &S, f3 d, float tmax, f
 }
 
 // HomogeneousMedium::Sample distance part, homogeneous.cpp:50-60 (two draws)
-__device__ __forceinline__ bool medium_sample(const DevScene &S, Pcg &rng, f3 d, float tmax, float &t) {
-    int ch = (int)(pcg_float(rng) * 3);
+template <class Smp>
+__device__ __forceinline__ bool medium_sample(const DevScene &S, Smp &rng, f3 d, float tmax, float &t) {
+    int ch = (int)(smp_1d(rng) * 3);
     ch = (2 < ch) ? 2 : ch;  // std::min(ch, 2)
     const float st = ch == 0 ? S.sigma_t[0] : (ch == 1 ? S.sigma_t[1] : S.sigma_t[2]);
-    const float dist = -bre_logf(1 - pcg_float(rng)) / st;
+    const float dist = -bre_logf(1 - smp_1d(rng)) / st;
     t = smin(dist * len3(d), tmax);
     return t < tmax;
+}
+
+// ---- GridDensityMedium (src/media/grid.{h,cpp}) ----
+BRE_TD float lerp_ref(float t, float v1, float v2) { return (1 - t) * v1 + t * v2; }  // pbrt.h:391
+
+// GridDensityMedium::D, grid.h:84-88 (0 outside [0, n) per axis)
+__device__ __forceinline__ float grid_D(const DevScene &S, int x, int y, int z) {
+    if (!(x >= 0 && x < S.gn[0] && y >= 0 && y < S.gn[1] && z >= 0 && z < S.gn[2])) return 0.f;
+    return S.density[((int64_t)z * S.gn[1] + y) * S.gn[0] + x];
+}
+
+// GridDensityMedium::Density, grid.cpp:46-60: trilinear over the sample lattice at cell centres
+__device__ __forceinline__ float grid_density(const DevScene &S, f3 p) {
+    const float sx = p.x * (float)S.gn[0] - .5f, sy = p.y * (float)S.gn[1] - .5f, sz = p.z * (float)S.gn[2] - .5f;
+    const int ix = (int)floorf(sx), iy = (int)floorf(sy), iz = (int)floorf(sz);
+    const float dx = sx - (float)ix, dy = sy - (float)iy, dz = sz - (float)iz;
+    const float d00 = lerp_ref(dx, grid_D(S, ix, iy, iz), grid_D(S, ix + 1, iy, iz));
+    const float d10 = lerp_ref(dx, grid_D(S, ix, iy + 1, iz), grid_D(S, ix + 1, iy + 1, iz));
+    const float d01 = lerp_ref(dx, grid_D(S, ix, iy, iz + 1), grid_D(S, ix + 1, iy, iz + 1));
+    const float d11 = lerp_ref(dx, grid_D(S, ix, iy + 1, iz + 1), grid_D(S, ix + 1, iy + 1, iz + 1));
+    const float d0 = lerp_ref(dy, d00, d10);
+    const float d1 = lerp_ref(dy, d01, d11);
+    return lerp_ref(dz, d0, d1);
+}
+
+// WorldToMedium(Ray(o, Normalize(d), tMax * |d|)) (grid.cpp:66-67) through
+// Transform::operator()(Ray) (transform.h:251-264, point with error bound :278-299, vector :236-242),
+// then Bounds3f(0, 1)::IntersectP(ray, &t0, &t1) (geometry.h:1386-1408).  Returns false on a miss.
+__device__ __forceinline__ bool grid_ray(const DevScene &S, f3 o, f3 d, float tmax, f3 &mo, f3 &md, float &t0,
+                                         float &t1) {
+    const f3 dn = normalize3(d);
+    const float tm = tmax * len3(d);
+    const float *m = S.w2m;
+    const float xp = m[0] * o.x + m[1] * o.y + m[2] * o.z + m[3];
+    const float yp = m[4] * o.x + m[5] * o.y + m[6] * o.z + m[7];
+    const float zp = m[8] * o.x + m[9] * o.y + m[10] * o.z + m[11];
+    const float wp = m[12] * o.x + m[13] * o.y + m[14] * o.z + m[15];
+    const float xs = fabsf(m[0] * o.x) + fabsf(m[1] * o.y) + fabsf(m[2] * o.z) + fabsf(m[3]);
+    const float ys = fabsf(m[4] * o.x) + fabsf(m[5] * o.y) + fabsf(m[6] * o.z) + fabsf(m[7]);
+    const float zs = fabsf(m[8] * o.x) + fabsf(m[9] * o.y) + fabsf(m[10] * o.z) + fabsf(m[11]);
+    const float g3 = gamma_n(3);
+    const f3 oerr = mk(g3 * xs, g3 * ys, g3 * zs);
+    f3 po = mk(xp, yp, zp);
+    if (!(wp == 1)) {
+        const float inv = (float)1 / wp;
+        po = mk(inv * xp, inv * yp, inv * zp);
+    }
+    const f3 dv = mk(m[0] * dn.x + m[1] * dn.y + m[2] * dn.z, m[4] * dn.x + m[5] * dn.y + m[6] * dn.z,
+                     m[8] * dn.x + m[9] * dn.y + m[10] * dn.z);
+    float rt = tm;
+    const float l2 = lensq3(dv);
+    if (l2 > 0) {
+        const float dt = dot3(abs3(dv), oerr) / l2;
+        po = add3(po, scale3(dv, dt));
+        rt -= dt;
+    }
+    mo = po;
+    md = dv;
+    float a = 0, b = rt;
+    const float pad = 1 + 2 * gamma_n(3);
+    const float oo[3] = {po.x, po.y, po.z}, dd[3] = {dv.x, dv.y, dv.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float inv = 1 / dd[i];
+        float tn = (0.f - oo[i]) * inv;
+        float tf = (1.f - oo[i]) * inv;
+        if (tn > tf) {
+            const float x = tn;
+            tn = tf;
+            tf = x;
+        }
+        tf *= pad;
+        a = tn > a ? tn : a;
+        b = tf < b ? tf : b;
+        if (a > b) return false;
+    }
+    t0 = a;
+    t1 = b;
+    return true;
+}
+
+// GridDensityMedium::Sample, grid.cpp:62-89: delta tracking.  On an interaction, t is the
+// medium-space distance and the interaction point is rWorld(t) = o + d*t (as the reference).
+template <class Smp>
+__device__ __forceinline__ bool grid_sample(const DevScene &S, Smp &smp, f3 o, f3 d, float tmax, float &t_out) {
+    f3 mo, md;
+    float tmin, tm;
+    if (!grid_ray(S, o, d, tmax, mo, md, tmin, tm)) return false;
+    float t = tmin;
+    while (true) {
+        t -= bre_logf(1 - smp_1d(smp)) * S.grid_inv_max / S.grid_sigma_t;
+        if (t >= tm) break;
+        if (grid_density(S, ray_at(mo, md, t)) * S.grid_inv_max > smp_1d(smp)) {
+            t_out = t;
+            return true;
+        }
+    }
+    return false;
+}
+
+// GridDensityMedium::Tr, grid.cpp:91-118: ratio tracking with Russian roulette below 0.1
+template <class Smp>
+__device__ __forceinline__ float grid_tr(const DevScene &S, Smp &smp, f3 o, f3 d, float tmax) {
+    f3 mo, md;
+    float tmin, tm;
+    if (!grid_ray(S, o, d, tmax, mo, md, tmin, tm)) return 1.f;
+    float tr = 1, t = tmin;
+    while (true) {
+        t -= bre_logf(1 - smp_1d(smp)) * S.grid_inv_max / S.grid_sigma_t;
+        if (t >= tm) break;
+        const float density = grid_density(S, ray_at(mo, md, t));
+        tr *= 1 - smax(0.f, density * S.grid_inv_max);
+        const float rr = 0.1f;
+        if (tr < rr) {
+            const float q = smax(0.05f, 1 - tr);
+            if (smp_1d(smp) < q) return 0.f;
+            tr /= 1 - q;
+        }
+    }
+    return tr;
+}
+
+// Medium::Tr of the world ray (o, d, tmax) for either medium type
+template <class Smp>
+__device__ __forceinline__ void medium_tr_any(const DevScene &S, Smp &smp, f3 o, f3 d, float tmax, float tr[3]) {
+    if (S.medium == BRE_MEDIUM_GRID) {
+        const float t = grid_tr(S, smp, o, d, tmax);
+        tr[0] = tr[1] = tr[2] = t;
+    } else {
+        medium_tr(S, d, tmax, tr);
+    }
+}
+
+// Medium::Sample distance decision; on true the interaction point is o + d*t
+template <class Smp>
+__device__ __forceinline__ bool medium_sample_any(const DevScene &S, Smp &smp, f3 o, f3 d, float tmax, float &t) {
+    if (S.medium == BRE_MEDIUM_GRID) return grid_sample(S, smp, o, d, tmax, t);
+    return medium_sample(S, smp, d, tmax, t);
 }
 
 BRE_TD bool black3(const float v[3]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
 BRE_TD float lum3(const float v[3]) { return 0.212671f * v[0] + 0.715160f * v[1] + 0.072169f * v[2]; }
 
 // ---- camera pass (bre_camera.hip) ----
-constexpr int kHaltonDims = 256;  // Halton dimensions with permutation tables (paths use <= 133)
+constexpr int kHaltonDims = 1000;  // HaltonSampler's PrimeTableSize = AwesomeSampler's limit (photonbeam.cpp:460)
 
 struct DevCamera {
     f3 pos, dir, right, nup;           // LookAt frame

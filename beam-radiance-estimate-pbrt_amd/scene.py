@@ -10,6 +10,7 @@ import ctypes
 
 MAX_QUADS = 64
 MAX_DEPTH = 16
+MEDIUM_NONE, MEDIUM_HOMOGENEOUS, MEDIUM_GRID = 0, 1, 2
 
 F3 = ctypes.c_float * 3
 
@@ -22,7 +23,9 @@ class Scene(ctypes.Structure):
     _fields_ = [("n_quads", ctypes.c_int32), ("light_quad", ctypes.c_int32), ("light_L", F3),
                 ("has_medium", ctypes.c_int32), ("sigma_a", F3), ("sigma_s", F3), ("g", ctypes.c_float),
                 ("cam_pos", F3), ("cam_look", F3), ("cam_up", F3), ("cam_fov_deg", ctypes.c_float),
-                ("quads", Quad * MAX_QUADS)]
+                ("quads", Quad * MAX_QUADS),
+                ("grid_n", ctypes.c_int32 * 3), ("world_to_medium", ctypes.c_float * 16),
+                ("grid_density", ctypes.c_void_p)]
 
     def to_bytes(self) -> bytes:
         return ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self))
@@ -92,3 +95,40 @@ def cornell_quads():
 def cornell_scene(sigma_a: float = 0.05, sigma_s: float = 0.5, g: float = 0.0) -> Scene:
     """Cornell box in homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)."""
     return make_scene(cornell_quads(), 6, (17.0, 12.0, 4.0), sigma_a, sigma_s, g)
+
+
+def smoke_density(n: int = 64, seed: int = 7):
+    """bre_smoke_density: seeded value-noise smoke (n^3 float32, x fastest), from libbre's host code."""
+    import numpy as np
+
+    from . import load_library
+
+    lib = load_library()
+    out = np.zeros(n * n * n, np.float32)
+    lib.bre_smoke_density(ctypes.c_int32(n), ctypes.c_uint64(seed), out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def grid_medium(scene: Scene, density, n, world_to_medium=None) -> Scene:
+    """Turn `scene`'s medium into a GridDensityMedium over `density` (n = (nx, ny, nz) or int).
+    The array is kept alive on the scene object (the struct only holds its address)."""
+    import numpy as np
+
+    nx, ny, nz = (n, n, n) if isinstance(n, int) else tuple(n)
+    dens = np.ascontiguousarray(density, np.float32).reshape(-1)
+    assert dens.shape[0] == nx * ny * nz
+    scene.has_medium = MEDIUM_GRID
+    scene.grid_n = (ctypes.c_int32 * 3)(nx, ny, nz)
+    m = np.eye(4, dtype=np.float32) if world_to_medium is None else np.asarray(world_to_medium, np.float32)
+    scene.world_to_medium = (ctypes.c_float * 16)(*[float(v) for v in m.reshape(-1)])
+    scene.grid_density = dens.ctypes.data
+    scene._density_ref = dens
+    return scene
+
+
+def cornell_smoke_scene(sigma_a: float = 0.5, sigma_s: float = 4.5, g: float = 0.7, n: int = 64, seed: int = 7,
+                        density=None) -> Scene:
+    """the Cornell box filled (on its unit cube) with a GridDensityMedium of
+    seeded value-noise smoke (bre_smoke_density(n, seed)), spectrally uniform sigma_t, HG g."""
+    s = cornell_scene(sigma_a, sigma_s, g)
+    return grid_medium(s, smoke_density(n, seed) if density is None else density, n)

@@ -29,9 +29,11 @@
 //     RasterToCamera / CameraToWorld matrix chain: the same ray up to float rounding of the
 //     matrix products, with the origin offset of Transform::operator()(Ray).  The same
 //     arithmetic is the product's contract (DESIGN.md "Camera pass").
-//   * Halton permutation tables are generated for the first 256 dimensions (a camera path of
-//     maxdepth <= 16 uses at most 5 + 16*8 = 133); the AwesomeSampler never reaches its 1000-
-//     dimension switch to PCG32 at these depths.
+//   * Halton permutation tables cover all 1000 prime dimensions.  Past its 1000th draw the
+//     AwesomeSampler switches to PCG32 sequence GoodPixelIndex = iterNumPixels++ (photonbeam.cpp:
+//     457-458), a counter the reference's camera-pass threads bump without synchronisation; this
+//     restatement takes the single-threaded ParallelFor2D order (tiles row-major, pixels x-fastest).
+//     Only GridDensityMedium paths (ratio tracking draws) get anywhere near 1000 draws.
 //   * The reference adds gather and surface terms to one pixel.Ld in path order; this
 //     restatement returns them separately (segments for the gather, surface radiance per pixel).
 //
@@ -43,7 +45,7 @@
 
 namespace orp {
 
-static const int kHaltonDims = 256;
+static const int kHaltonDims = 1000;  // PrimeTableSize (lowdiscrepancy.h:38) = AwesomeSampler's limit
 static const Float ShadowEpsilon = 0.0001f;
 
 // ---- low-discrepancy primitives ----
@@ -198,27 +200,30 @@ struct Halton {
 };
 
 // AwesomeSampler(0, haltonTileSampler, 1000, GoodPixelIndex) after StartPixel + SetSampleNumber(iter)
+// (photonbeam.cpp:188-224, 456-462; GlobalSampler::Get1D/Get2D, sampler.cpp:178-195)
 struct CameraSampler {
     const Halton *h;
     int64_t index;
-    int dim = 0;
-    bool overflow = false;
+    int dimension = 0;
+    size_t sampleCount = 0;
+    RNG rng;
     Float Get1D() {
-        if (dim >= kHaltonDims) {
-            overflow = true;
-            return 0;
-        }
-        return h->SampleDimension(index, dim++);
+        sampleCount++;
+        if (sampleCount <= (size_t)kHaltonDims) return h->SampleDimension(index, dimension++);
+        return rng.UniformFloat();
     }
     void Get2D(Float *x, Float *y) {
-        if (dim + 1 >= kHaltonDims) {
-            overflow = true;
-            *x = *y = 0;
+        sampleCount += 2;
+        if (sampleCount <= (size_t)kHaltonDims) {
+            *x = h->SampleDimension(index, dimension);
+            *y = h->SampleDimension(index, dimension + 1);
+            dimension += 2;
             return;
         }
-        *x = h->SampleDimension(index, dim);
-        *y = h->SampleDimension(index, dim + 1);
-        dim += 2;
+        Float first = rng.UniformFloat();  // Point2f(rng.UniformFloat(), rng.UniformFloat()), right to left
+        Float second = rng.UniformFloat();
+        *x = second;
+        *y = first;
     }
 };
 
@@ -318,7 +323,7 @@ struct Interaction {
     int quad;
 };
 
-static Spectrum VisibilityTr(const Scene &sc, const Interaction &p0, const Interaction &p1) {
+static Spectrum VisibilityTr(const Scene &sc, const Interaction &p0, const Interaction &p1, CameraSampler &cs) {
     Ray ray;
     ray.o = OffsetRayOrigin(p0.p, p0.pError, p0.n, p1.p - p0.p);
     V3 target = OffsetRayOrigin(p1.p, p1.pError, p1.n, ray.o - p1.p);
@@ -328,11 +333,12 @@ static Spectrum VisibilityTr(const Scene &sc, const Interaction &p0, const Inter
     Isect isect;
     bool hit = Intersect(sc, ray, &isect);
     if (hit) return Spectrum(0.0f);  // every quad has a material
-    if (sc.medium) Tr = Tr * MediumTr(sc, ray);
+    if (sc.medium) Tr = Tr * MediumTr(sc, ray, cs);
     return Tr;
 }
 
-static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx, Float usy, Float ulx, Float uly) {
+static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx, Float usy, Float ulx, Float uly,
+                               CameraSampler &cs) {
     const Quad &L = sc.quads[sc.light];
     const Quad &q = sc.quads[it.quad];
     Spectrum Ld(0.f);
@@ -364,7 +370,7 @@ static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx
         Spectrum f = BSDF_f(q, it.wo, wi) * AbsDot(wi, q.n);
         scatteringPdf = BSDF_Pdf(q, it.wo, wi);
         if (!f.IsBlack()) {
-            Li = Li * VisibilityTr(sc, it, pS);
+            Li = Li * VisibilityTr(sc, it, pS, cs);
             if (!Li.IsBlack()) {
                 Float weight = PowerHeuristic(1, lightPdf, 1, scatteringPdf);
                 Ld = Ld + f * Li * weight / lightPdf;
@@ -396,7 +402,7 @@ static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx
             Spectrum Tr(1.f);
             Isect li;
             bool found = Intersect(sc, r2, &li);
-            if (sc.medium) Tr = Tr * MediumTr(sc, r2);
+            if (sc.medium) Tr = Tr * MediumTr(sc, r2, cs);
             Spectrum Lr(0.f);
             if (found && li.quad == sc.light) Lr = Dot(li.n, -wi) > 0 ? sc.Lemit : Spectrum(0.f);
             if (!Lr.IsBlack()) Ld = Ld + f * Lr * Tr * weight / scatteringPdf;
@@ -414,11 +420,12 @@ struct Segment {
 // One camera path (photonbeam.cpp:456-553).  Returns false if the path needed more Halton
 // dimensions than the table holds.
 static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int px, int py, int width, int iter,
-                       int maxDepth, bool renderSurfaces, bool renderMedia, std::vector<Segment> &segs,
-                       Spectrum *Ld) {
+                       int maxDepth, bool renderSurfaces, bool renderMedia, uint64_t goodPixelIndex,
+                       std::vector<Segment> &segs, Spectrum *Ld) {
     CameraSampler cs;
     cs.h = &h;
     cs.index = h.IndexForSample(px, py, iter);
+    cs.rng = RNG(goodPixelIndex);
     Float fx, fy, lx, ly;
     cs.Get2D(&fx, &fy);
     fx = (Float)px + fx;
@@ -434,7 +441,7 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
         ray.tMax = Infinity;
         if (!Intersect(sc, ray, &isect)) break;  // area lights have no Le(ray)
         Spectrum mediumBeta(1.0f);
-        if (sc.medium) mediumBeta = MediumTr(sc, ray);
+        if (sc.medium) mediumBeta = MediumTr(sc, ray, cs);
         if (renderMedia) segs.push_back(Segment{ray.o, isect.p, ray.d, ray.tMax, pixel, depth});
         beta = beta * mediumBeta;
         if (!renderSurfaces) break;  // every quad has a BSDF
@@ -453,7 +460,7 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
         it.n = isect.n;
         it.wo = Normalize(wo);
         it.quad = isect.quad;
-        *Ld = *Ld + beta * (EstimateDirect(sc, it, usx, usy, ulx, uly) / Float(1));
+        *Ld = *Ld + beta * (EstimateDirect(sc, it, usx, usy, ulx, uly, cs) / Float(1));
         if (depth < maxDepth - 1) {
             Float ux, uy, pdf = 0;
             cs.Get2D(&ux, &uy);
@@ -471,7 +478,7 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
             beta = beta / continueProb;
         }
     }
-    return !cs.overflow;
+    return true;
 }
 
 }  // namespace orp
@@ -488,6 +495,20 @@ int64_t ora_camera_pass(const bre_scene *scene, int32_t width, int32_t height, i
     orp::Scene sc = orp::make_scene(scene);
     orp::Camera cam = orp::make_camera(scene, width, height);
     orp::Halton h(width, height);
+    // GoodPixelIndex of each pixel: ParallelFor2D's serial order over 16x16 tiles, then the tile's
+    // Bounds2i iteration (photonbeam.cpp:444-458)
+    std::vector<uint64_t> good((size_t)width * height);
+    {
+        const int tileSize = 16, ntx = (width + tileSize - 1) / tileSize, nty = (height + tileSize - 1) / tileSize;
+        uint64_t counter = 0;
+        for (int ty = 0; ty < nty; ++ty)
+            for (int tx = 0; tx < ntx; ++tx) {
+                int x0 = tx * tileSize, x1 = std::min(x0 + tileSize, width);
+                int y0 = ty * tileSize, y1 = std::min(y0 + tileSize, height);
+                for (int y = y0; y < y1; ++y)
+                    for (int x = x0; x < x1; ++x) good[(size_t)y * width + x] = counter++;
+            }
+    }
     std::vector<orp::Segment> segs;
     int64_t total = 0;
     for (int py = 0; py < height; ++py) {
@@ -495,7 +516,7 @@ int64_t ora_camera_pass(const bre_scene *scene, int32_t width, int32_t height, i
             segs.clear();
             orp::Spectrum Ld(0.f);
             if (!orp::CameraPath(sc, cam, h, px, py, width, iteration, max_depth, render_surfaces != 0,
-                                 render_media != 0, segs, &Ld))
+                                 render_media != 0, good[(size_t)py * width + px], segs, &Ld))
                 return -1;
             if (ld_rgb)
                 for (int c = 0; c < 3; ++c) ld_rgb[3 * (py * width + px) + c] += Ld.c[c];

@@ -19,6 +19,9 @@
 //   * OffsetRayOrigin / NextFloatUp/Down                       src/core/geometry.h:1438-1458,
 //                                                               src/core/pbrt.h (NextFloatUp/Down)
 //   * HomogeneousMedium::Tr / Sample    src/media/homogeneous.cpp:44-77
+//   * GridDensityMedium::Density / Sample / Tr           src/media/grid.cpp:46-118, grid.h:58-88
+//     (WorldToMedium through Transform::operator()(Ray), transform.h:236-299; Bounds3::IntersectP
+//     with t0/t1, geometry.h:1386-1408)
 //   * HenyeyGreenstein::Sample_p / p, PhaseHG                  src/core/medium.cpp:194-218, medium.h:69-72
 //   * BSDF::Sample_f (one Lambertian BxDF), BxDF::Sample_f     src/core/reflection.cpp:378-389, 703-768
 //   * Spectrum (RGB) y(), Exp, operator/ (true division)       src/core/spectrum.h:181-194, 222-227, 462-465
@@ -71,10 +74,10 @@ static void TraceRecursive(Ray photonRay, int depth, Spectrum beta, Sampler &sam
             scattered.o = photonRay(tScatter);  // MediumInteraction::SpawnRay: no offset
             scattered.d = wi;
             scattered.tMax = Infinity;
-            Spectrum scatteredBeta = beta * MediumTr(sc, photonRay);
+            Spectrum scatteredBeta = beta * MediumTr(sc, photonRay, sampler);
             TraceRecursive(scattered, depth + 1, scatteredBeta, sampler, sc, MaxDepth, BeamRadius, out);
         }
-        if (sc.medium) betaMedium = MediumTr(sc, photonRay);
+        if (sc.medium) betaMedium = MediumTr(sc, photonRay, sampler);
         Beam b;
         b.start = photonRay.o;
         b.end = isect.p;
@@ -225,7 +228,7 @@ void ora_homogeneous_tr(const float *sigma_a, const float *sigma_s, int64_t n, c
         orp::Ray r;
         r.d = orp::V3(d + 3 * i);
         r.tMax = tmax[i];
-        orp::Spectrum t = orp::MediumTr(sc, r);
+        orp::Spectrum t = orp::HomogeneousTr(sc, r);
         for (int k = 0; k < 3; ++k) tr[3 * i + k] = t.c[k];
     }
 }
@@ -250,6 +253,47 @@ void ora_fmath(int32_t kind, int64_t n, const float *x, float *y) {
             case 2: bre_sincosf(x[i], &s, &c); y[i] = s; break;
             default: bre_sincosf(x[i], &s, &c); y[i] = c; break;
         }
+    }
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// GridDensityMedium::Density at n medium-space points p[3n] (grid.cpp:46-60)
+void ora_grid_density(const bre_scene *scene, int64_t n, const float *p, float *out) {
+    orp::Scene sc = orp::make_scene(scene);
+    for (int64_t i = 0; i < n; ++i) out[i] = orp::GridDensity(sc, orp::V3(p + 3 * i));
+}
+
+// GridDensityMedium::Tr (kind 0) or ::Sample (kind 1; out = medium-space t or -1 when no
+// interaction) for n world rays, ray i drawing from PCG32 sequence seq0 + i; draws[i] = number of
+// sampler draws it used
+void ora_grid_eval(const bre_scene *scene, int32_t kind, int64_t n, const float *o, const float *d,
+                   const float *tmax, uint64_t seq0, float *out, int32_t *draws) {
+    orp::Scene sc = orp::make_scene(scene);
+    struct Counting {
+        orp::Sampler s;
+        int32_t n = 0;
+        explicit Counting(uint64_t q) : s(q) {}
+        orp::Float Get1D() {
+            ++n;
+            return s.Get1D();
+        }
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        orp::Ray r;
+        r.o = orp::V3(o + 3 * i);
+        r.d = orp::V3(d + 3 * i);
+        r.tMax = tmax[i];
+        Counting cs(seq0 + (uint64_t)i);
+        if (kind == 0) {
+            out[i] = orp::GridTr(sc, r, cs).c[0];
+        } else {
+            orp::Float t = 0;
+            out[i] = orp::GridSample(sc, r, cs, &t) ? t : -1.f;
+        }
+        if (draws) draws[i] = cs.n;
     }
 }
 

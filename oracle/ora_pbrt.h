@@ -231,6 +231,12 @@ struct Scene {
     bool medium;
     Spectrum sigma_t, sigma_s;
     Float g;
+    // GridDensityMedium (grid.h:50-100)
+    bool grid = false;
+    int nx = 0, ny = 0, nz = 0;
+    Float m[4][4];  // WorldToMedium
+    const float *density = nullptr;
+    Float gridSigmaT = 0, invMaxDensity = 0;
 };
 
 static Scene make_scene(const bre_scene *s) {
@@ -258,6 +264,19 @@ static Scene make_scene(const bre_scene *s) {
     sc.sigma_s = Spectrum(s->sigma_s);
     sc.sigma_t = sa + sc.sigma_s;
     sc.g = s->g;
+    if (s->has_medium == BRE_MEDIUM_GRID) {
+        sc.grid = true;
+        sc.nx = s->grid_n[0];
+        sc.ny = s->grid_n[1];
+        sc.nz = s->grid_n[2];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) sc.m[i][j] = s->world_to_medium[4 * i + j];
+        sc.density = s->grid_density;
+        sc.gridSigmaT = (sa + sc.sigma_s).c[0];
+        Float maxDensity = 0;
+        for (int i = 0; i < sc.nx * sc.ny * sc.nz; ++i) maxDensity = std::max(maxDensity, sc.density[i]);
+        sc.invMaxDensity = 1 / maxDensity;
+    }
     return sc;
 }
 
@@ -302,17 +321,138 @@ static bool Intersect(const Scene &sc, Ray &ray, Isect *isect) {
 }
 
 // HomogeneousMedium (homogeneous.cpp:44-77)
-static Spectrum MediumTr(const Scene &sc, const Ray &ray) {
+static Spectrum HomogeneousTr(const Scene &sc, const Ray &ray) {
     return Exp(-sc.sigma_t * std::min(ray.tMax * ray.d.Length(), MaxFloat));
 }
 // returns sampledMedium; *t = sampled distance.  (The returned weight is unused by the photon
 // tracer, which overwrites betaMedium with Tr, photonbeam.cpp:289.)
-static bool MediumSample(const Scene &sc, const Ray &ray, Sampler &sampler, Float *tOut) {
+template <class S>
+static bool HomogeneousSample(const Scene &sc, const Ray &ray, S &sampler, Float *tOut) {
     int channel = std::min((int)(sampler.Get1D() * 3), 3 - 1);
     Float dist = -bre_logf(1 - sampler.Get1D()) / sc.sigma_t.c[channel];
     Float t = std::min(dist * ray.d.Length(), ray.tMax);
     *tOut = t;
     return t < ray.tMax;
+}
+
+// ---- GridDensityMedium (grid.h:84-88, grid.cpp:46-118) ----
+static inline Float Lerp(Float t, Float v1, Float v2) { return (1 - t) * v1 + t * v2; }
+static Float GridD(const Scene &sc, int x, int y, int z) {
+    // InsideExclusive(p, Bounds3i((0,0,0), (nx,ny,nz)))
+    if (!(x >= 0 && x < sc.nx && y >= 0 && y < sc.ny && z >= 0 && z < sc.nz)) return 0;
+    return sc.density[(z * sc.ny + y) * sc.nx + x];
+}
+static Float GridDensity(const Scene &sc, const V3 &p) {
+    V3 ps(p.x * sc.nx - .5f, p.y * sc.ny - .5f, p.z * sc.nz - .5f);
+    int pi[3] = {(int)std::floor(ps.x), (int)std::floor(ps.y), (int)std::floor(ps.z)};
+    V3 d(ps.x - (Float)pi[0], ps.y - (Float)pi[1], ps.z - (Float)pi[2]);
+    Float d00 = Lerp(d.x, GridD(sc, pi[0], pi[1], pi[2]), GridD(sc, pi[0] + 1, pi[1], pi[2]));
+    Float d10 = Lerp(d.x, GridD(sc, pi[0], pi[1] + 1, pi[2]), GridD(sc, pi[0] + 1, pi[1] + 1, pi[2]));
+    Float d01 = Lerp(d.x, GridD(sc, pi[0], pi[1], pi[2] + 1), GridD(sc, pi[0] + 1, pi[1], pi[2] + 1));
+    Float d11 = Lerp(d.x, GridD(sc, pi[0], pi[1] + 1, pi[2] + 1), GridD(sc, pi[0] + 1, pi[1] + 1, pi[2] + 1));
+    Float d0 = Lerp(d.y, d00, d10);
+    Float d1 = Lerp(d.y, d01, d11);
+    return Lerp(d.z, d0, d1);
+}
+// Transform::operator()(const Ray &) (transform.h:251-264) with the point transform and its error
+// bound (:278-299) and the vector transform (:236-242)
+static Ray TransformRay(const Float m[4][4], const Ray &r) {
+    Float x = r.o.x, y = r.o.y, z = r.o.z;
+    Float xp = m[0][0] * x + m[0][1] * y + m[0][2] * z + m[0][3];
+    Float yp = m[1][0] * x + m[1][1] * y + m[1][2] * z + m[1][3];
+    Float zp = m[2][0] * x + m[2][1] * y + m[2][2] * z + m[2][3];
+    Float wp = m[3][0] * x + m[3][1] * y + m[3][2] * z + m[3][3];
+    Float xAbsSum = (std::abs(m[0][0] * x) + std::abs(m[0][1] * y) + std::abs(m[0][2] * z) + std::abs(m[0][3]));
+    Float yAbsSum = (std::abs(m[1][0] * x) + std::abs(m[1][1] * y) + std::abs(m[1][2] * z) + std::abs(m[1][3]));
+    Float zAbsSum = (std::abs(m[2][0] * x) + std::abs(m[2][1] * y) + std::abs(m[2][2] * z) + std::abs(m[2][3]));
+    V3 oError = V3(xAbsSum, yAbsSum, zAbsSum) * gamma(3);
+    V3 o = (wp == 1) ? V3(xp, yp, zp) : V3(xp, yp, zp) * ((Float)1 / wp);
+    V3 d(m[0][0] * r.d.x + m[0][1] * r.d.y + m[0][2] * r.d.z, m[1][0] * r.d.x + m[1][1] * r.d.y + m[1][2] * r.d.z,
+         m[2][0] * r.d.x + m[2][1] * r.d.y + m[2][2] * r.d.z);
+    Float lengthSquared = d.LengthSquared();
+    Float tMax = r.tMax;
+    if (lengthSquared > 0) {
+        Float dt = Dot(Abs(d), oError) / lengthSquared;
+        o = o + d * dt;
+        tMax -= dt;
+    }
+    Ray out;
+    out.o = o;
+    out.d = d;
+    out.tMax = tMax;
+    return out;
+}
+// Bounds3f((0,0,0), (1,1,1)).IntersectP(ray, &t0, &t1), geometry.h:1386-1408
+static bool UnitBoxIntersectP(const Ray &ray, Float *hitt0, Float *hitt1) {
+    Float t0 = 0, t1 = ray.tMax;
+    for (int i = 0; i < 3; ++i) {
+        Float invRayDir = 1 / ray.d[i];
+        Float tNear = ((Float)0 - ray.o[i]) * invRayDir;
+        Float tFar = ((Float)1 - ray.o[i]) * invRayDir;
+        if (tNear > tFar) std::swap(tNear, tFar);
+        tFar *= 1 + 2 * gamma(3);
+        t0 = tNear > t0 ? tNear : t0;
+        t1 = tFar < t1 ? tFar : t1;
+        if (t0 > t1) return false;
+    }
+    *hitt0 = t0;
+    *hitt1 = t1;
+    return true;
+}
+static Ray GridMediumRay(const Scene &sc, const Ray &rWorld) {
+    Ray r;
+    r.o = rWorld.o;
+    r.d = Normalize(rWorld.d);
+    r.tMax = rWorld.tMax * rWorld.d.Length();
+    return TransformRay(sc.m, r);
+}
+// GridDensityMedium::Sample (grid.cpp:62-89): delta tracking; the interaction is at rWorld(t)
+template <class S>
+static bool GridSample(const Scene &sc, const Ray &rWorld, S &sampler, Float *tOut) {
+    Ray ray = GridMediumRay(sc, rWorld);
+    Float tMin, tMax;
+    if (!UnitBoxIntersectP(ray, &tMin, &tMax)) return false;
+    Float t = tMin;
+    while (true) {
+        t -= bre_logf(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
+        if (t >= tMax) break;
+        if (GridDensity(sc, ray(t)) * sc.invMaxDensity > sampler.Get1D()) {
+            *tOut = t;
+            return true;
+        }
+    }
+    return false;
+}
+// GridDensityMedium::Tr (grid.cpp:91-118): ratio tracking with Russian roulette below 0.1
+template <class S>
+static Spectrum GridTr(const Scene &sc, const Ray &rWorld, S &sampler) {
+    Ray ray = GridMediumRay(sc, rWorld);
+    Float tMin, tMax;
+    if (!UnitBoxIntersectP(ray, &tMin, &tMax)) return Spectrum(1.f);
+    Float Tr = 1, t = tMin;
+    while (true) {
+        t -= bre_logf(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
+        if (t >= tMax) break;
+        Float density = GridDensity(sc, ray(t));
+        Tr *= 1 - std::max((Float)0, density * sc.invMaxDensity);
+        const Float rrThreshold = .1;
+        if (Tr < rrThreshold) {
+            Float q = std::max((Float).05, 1 - Tr);
+            if (sampler.Get1D() < q) return Spectrum(0.f);
+            Tr /= 1 - q;
+        }
+    }
+    return Spectrum(Tr);
+}
+
+// Medium::Tr / Medium::Sample of the scene's medium
+template <class S>
+static Spectrum MediumTr(const Scene &sc, const Ray &ray, S &sampler) {
+    return sc.grid ? GridTr(sc, ray, sampler) : HomogeneousTr(sc, ray);
+}
+template <class S>
+static bool MediumSample(const Scene &sc, const Ray &ray, S &sampler, Float *tOut) {
+    return sc.grid ? GridSample(sc, ray, sampler, tOut) : HomogeneousSample(sc, ray, sampler, tOut);
 }
 
 }  // namespace orp

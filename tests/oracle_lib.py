@@ -58,6 +58,8 @@ class Oracle:
         lib.ora_scrambled_radical_inverse.argtypes = [I32, U64, P]
         lib.ora_scrambled_radical_inverse.restype = F
         lib.ora_shuffle.argtypes = [U64, I32, P]
+        lib.ora_grid_density.argtypes = [P, I64, P, P]
+        lib.ora_grid_eval.argtypes = [P, I32, I64, P, P, P, U64, P, P]
 
     # -- primitives --
     def slab_pad(self) -> float:
@@ -140,6 +142,23 @@ class Oracle:
         y = np.zeros_like(x)
         self.lib.ora_fmath({"log": 0, "exp": 1, "sin": 2, "cos": 3}[kind], x.shape[0], _p(x), _p(y))
         return y
+
+    # -- GridDensityMedium (oracle/ora_pbrt.h) --
+    def grid_density(self, scene, p):
+        p = np.ascontiguousarray(p, np.float32)
+        out = np.zeros(p.shape[0], np.float32)
+        self.lib.ora_grid_density(ctypes.addressof(scene), p.shape[0], _p(p), _p(out))
+        return out
+
+    def grid_eval(self, scene, kind, o, d, tmax, seq0=1):
+        """kind 'tr' -> Tr per ray; 'sample' -> medium-space t or -1; plus sampler draws used."""
+        o, d, tmax = (np.ascontiguousarray(x, np.float32) for x in (o, d, tmax))
+        n = tmax.shape[0]
+        out = np.zeros(n, np.float32)
+        draws = np.zeros(n, np.int32)
+        self.lib.ora_grid_eval(ctypes.addressof(scene), {"tr": 0, "sample": 1}[kind], n, _p(o), _p(d), _p(tmax),
+                               seq0, _p(out), _p(draws))
+        return out, draws
 
     # -- camera pass (oracle/bre_oracle_camera.cpp) --
     def camera_pass(self, scene, width, height, iteration=0, max_depth=5, render_surfaces=True, render_media=True):

@@ -8,6 +8,7 @@ same float32 arithmetic.  Slow (pure Python): used on a few hundred photons to p
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import struct
 
@@ -296,6 +297,17 @@ class Scene:
         self.medium = bool(s.has_medium)
         self.sigma_t = tuple(f32(f32(a) + f32(b)) for a, b in zip(s.sigma_a, s.sigma_s))
         self.g = f32(s.g)
+        self.grid = s.has_medium == 2
+        if self.grid:  # GridDensityMedium ctor, grid.h:58-77
+            self.n = tuple(int(v) for v in s.grid_n)
+            self.m = [[f32(s.world_to_medium[4 * i + j]) for j in range(4)] for i in range(4)]
+            cnt = self.n[0] * self.n[1] * self.n[2]
+            self.density = np.ctypeslib.as_array((ctypes.c_float * cnt).from_address(s.grid_density)).copy()
+            self.gsig = f32(f32(s.sigma_a[0]) + f32(s.sigma_s[0]))
+            mx = f32(0)
+            for v in self.density:
+                mx = v if mx < v else mx
+            self.inv_max = f32(f32(1) / mx)
 
     def intersect(self, o, d):
         best = None
@@ -323,6 +335,104 @@ class Scene:
         x = f32(tmax * length(d))
         x = MAXF if MAXF < x else x
         return tuple(expf(f32(f32(-st) * x)) for st in self.sigma_t)
+
+
+# ---- GridDensityMedium (grid.cpp:46-118; grid.h:84-88) ----
+def _lerp(t, a, b):
+    return f32(f32(f32(f32(1) - t) * a) + f32(t * b))
+
+
+def _grid_d(sc, x, y, z):
+    nx, ny, nz = sc.n
+    if not (0 <= x < nx and 0 <= y < ny and 0 <= z < nz):
+        return f32(0)
+    return sc.density[(z * ny + y) * nx + x]
+
+
+def _grid_density(sc, p):
+    ps = [f32(f32(p[i] * f32(sc.n[i])) - f32(0.5)) for i in range(3)]
+    pi = [int(math.floor(v)) for v in ps]
+    d = [f32(ps[i] - f32(pi[i])) for i in range(3)]
+    x, y, z = pi
+    d00 = _lerp(d[0], _grid_d(sc, x, y, z), _grid_d(sc, x + 1, y, z))
+    d10 = _lerp(d[0], _grid_d(sc, x, y + 1, z), _grid_d(sc, x + 1, y + 1, z))
+    d01 = _lerp(d[0], _grid_d(sc, x, y, z + 1), _grid_d(sc, x + 1, y, z + 1))
+    d11 = _lerp(d[0], _grid_d(sc, x, y + 1, z + 1), _grid_d(sc, x + 1, y + 1, z + 1))
+    return _lerp(d[2], _lerp(d[1], d00, d10), _lerp(d[1], d01, d11))
+
+
+def _grid_ray(sc, o, d, tmax):
+    """WorldToMedium(Ray(o, Normalize(d), tMax*|d|)) (transform.h:251-299) and the unit-box
+    IntersectP with t0/t1 (geometry.h:1386-1408); None on a miss."""
+    dn = normalize(d)
+    tm = f32(tmax * length(d))
+    m = sc.m
+    row = [f32(f32(f32(f32(m[i][0] * o[0]) + f32(m[i][1] * o[1])) + f32(m[i][2] * o[2])) + m[i][3]) for i in range(4)]
+    err = [f32(f32(f32(abs(f32(m[i][0] * o[0])) + abs(f32(m[i][1] * o[1]))) + abs(f32(m[i][2] * o[2]))) + abs(m[i][3]))
+           for i in range(3)]
+    g3 = gamma(3)
+    oerr = tuple(f32(g3 * e) for e in err)
+    po = tuple(row[:3])
+    if not (row[3] == 1):
+        inv = f32(f32(1) / row[3])
+        po = tuple(f32(inv * v) for v in po)
+    dv = tuple(f32(f32(f32(m[i][0] * dn[0]) + f32(m[i][1] * dn[1])) + f32(m[i][2] * dn[2])) for i in range(3))
+    l2 = dot(dv, dv)
+    if l2 > 0:
+        dt = f32(dot(vabs(dv), oerr) / l2)
+        po = add(po, mul(dv, dt))
+        tm = f32(tm - dt)
+    t0, t1 = f32(0), tm
+    pad = f32(f32(1) + f32(f32(2) * g3))
+    for i in range(3):
+        inv = f32(f32(1) / dv[i]) if dv[i] != 0 else f32(math.copysign(np.inf, dv[i]))
+        with np.errstate(invalid="ignore"):
+            tn = f32(f32(f32(0) - po[i]) * inv)
+            tf = f32(f32(f32(1) - po[i]) * inv)
+        if tn > tf:
+            tn, tf = tf, tn
+        tf = f32(tf * pad)
+        t0 = tn if tn > t0 else t0
+        t1 = tf if tf < t1 else t1
+        if t0 > t1:
+            return None
+    return po, dv, t0, t1
+
+
+def grid_sample(sc, rng, o, d, tmax):
+    """Delta tracking (grid.cpp:62-89): the medium-space t of the interaction, or None."""
+    r = _grid_ray(sc, o, d, tmax)
+    if r is None:
+        return None
+    mo, md, t, tm = r
+    while True:
+        t = f32(t - f32(f32(logf(f32(f32(1) - rng.uniform())) * sc.inv_max) / sc.gsig))
+        if t >= tm:
+            return None
+        if f32(_grid_density(sc, add(mo, mul(md, t))) * sc.inv_max) > rng.uniform():
+            return t
+
+
+def grid_tr(sc, rng, o, d, tmax):
+    """Ratio tracking with Russian roulette below 0.1 (grid.cpp:91-118)."""
+    r = _grid_ray(sc, o, d, tmax)
+    if r is None:
+        return f32(1)
+    mo, md, t, tm = r
+    tr = f32(1)
+    while True:
+        t = f32(t - f32(f32(logf(f32(f32(1) - rng.uniform())) * sc.inv_max) / sc.gsig))
+        if t >= tm:
+            return tr
+        dens = _grid_density(sc, add(mo, mul(md, t)))
+        x = f32(dens * sc.inv_max)
+        tr = f32(tr * f32(f32(1) - (x if f32(0) < x else f32(0))))
+        if tr < f32(0.1):
+            q = f32(f32(1) - tr)
+            q = q if f32(0.05) < q else f32(0.05)
+            if rng.uniform() < q:
+                return f32(0)
+            tr = f32(tr / f32(f32(1) - q))
 
 
 def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
@@ -358,7 +468,10 @@ def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
             if hit is None:
                 return
             scattered = False
-            if sc.medium:
+            if sc.medium and sc.grid:
+                t = grid_sample(sc, rng, o, d, tmax)
+                scattered = t is not None
+            elif sc.medium:
                 ch = min(int(f32(rng.uniform() * f32(3))), 2)
                 dist = f32(-logf(f32(f32(1) - rng.uniform())) / sc.sigma_t[ch])
                 dl = f32(dist * length(d))
@@ -369,9 +482,12 @@ def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
             if scattered:
                 hx, hy = rng.get2d()
                 wi = hg_sample(sc.g, tuple(-x for x in d), hx, hy)
-                trv = sc.tr(d, tmax)
+                trv = (grid_tr(sc, rng, o, d, tmax),) * 3 if sc.grid else sc.tr(d, tmax)
                 rec(add(o, mul(d, t)), wi, depth + 1, tuple(f32(b * x) for b, x in zip(beta, trv)))
-            bm = sc.tr(d, tmax) if sc.medium else (f32(1),) * 3
+            if sc.medium and sc.grid:
+                bm = (grid_tr(sc, rng, o, d, tmax),) * 3
+            else:
+                bm = sc.tr(d, tmax) if sc.medium else (f32(1),) * 3
             out.append((o, hit[0], f32(radius), tuple(f32(a * b) for a, b in zip(bm, beta))))
             q = sc.quads[hit[2]]
             ux, uy = rng.get2d()
@@ -429,8 +545,6 @@ def trace_photons(scene_struct, n_photons, iteration=0, max_depth=5, radius=0.01
     arr["counts"] = np.array(counts, np.int32)
     return arr
 
-
-del math
 
 
 # ---- HaltonSampler restated (src/samplers/halton.cpp:63-127, lowdiscrepancy.cpp) ----

@@ -215,3 +215,112 @@ def test_photon_pass_vacuum_and_depth(oracle, scene_mod):
     # renormalisation keeps luminance-weighted power constant when RR continues
     d1 = oracle.trace_photons(scene_mod.cornell_scene(), 5000, max_depth=1)
     assert d1["counts"].max() <= 1
+
+
+# ---------------- GridDensityMedium (grid.cpp:46-118) ----------------
+def _const_grid(scene_mod, value=1.0, n=4, sigma_a=0.5, sigma_s=1.5):
+    s = scene_mod.cornell_scene(sigma_a, sigma_s, 0.0)
+    return scene_mod.grid_medium(s, np.full(n ** 3, value, np.float32), n)
+
+
+def test_grid_density_trilinear_kat(oracle, scene_mod):
+    """Density is the trilinear interpolant of the samples at cell centres (grid.cpp:46-60), with
+    D = 0 outside [0, n) (grid.h:84-88)."""
+    n = 4
+    rng = np.random.default_rng(11)
+    dens = rng.random(n ** 3).astype(np.float32)
+    s = scene_mod.grid_medium(scene_mod.cornell_scene(), dens, n)
+    c = (np.arange(n, dtype=np.float32) + np.float32(0.5)) / np.float32(n)
+    z, y, x = np.meshgrid(c, c, c, indexing="ij")
+    pts = np.stack([x.ravel(), y.ravel(), z.ravel()], 1)
+    assert np.array_equal(oracle.grid_density(s, pts), dens)
+    # half a cell outside the lattice: lerp towards D = 0
+    edge = np.array([[0.0, c[1], c[1]], [1.0, c[2], c[2]]], np.float32)
+    got = oracle.grid_density(s, edge)
+    want = np.array([0.5 * dens[(1 * n + 1) * n + 0], 0.5 * dens[(2 * n + 2) * n + 3]], np.float32)
+    assert np.allclose(got, want, rtol=1e-6)
+    # far outside the box: zero
+    assert oracle.grid_density(s, np.array([[3.0, 0.5, 0.5], [-2.0, -2.0, -2.0]], np.float32)).tolist() == [0, 0]
+
+
+def test_grid_tr_unbiased_constant_density(oracle, scene_mod):
+    """Ratio tracking is unbiased: constant density 1, sigma_t 2, a ray crossing the unit cube
+    along x (medium length 1, inside the lattice's [0.5/n, 1-0.5/n] plateau the interpolant is
+    exactly 1; over the outer half cells it ramps to 0) -> mean Tr = exp(-2 * integral)."""
+    n = 8
+    s = _const_grid(scene_mod, 1.0, n, 0.5, 1.5)
+    m = 40000
+    o = np.tile(np.array([[-0.5, 0.5, 0.5]], np.float32), (m, 1))
+    d = np.tile(np.array([[1.0, 0.0, 0.0]], np.float32), (m, 1))
+    tr, draws = oracle.grid_eval(s, "tr", o, d, np.full(m, 2.0, np.float32))
+    # plateau between the first and last cell centres + two half-cell ramps from 1 to 0.5 (mean 0.75)
+    integral = 1 - 1.0 / n + 2 * (0.5 / n) * 0.75
+    want = np.exp(-2.0 * integral)
+    se = tr.std() / np.sqrt(m)
+    assert abs(tr.mean() - want) < 4 * se + 1e-4, (tr.mean(), want)
+    assert np.all((tr >= 0) & (tr <= 1.0 / 0.95 + 1e-6)) and draws.min() >= 1
+
+
+def test_grid_sample_escape_probability(oracle, scene_mod):
+    """Delta tracking: P(no interaction over the crossing) = exp(-sigma_t * integral of density)."""
+    n = 8
+    s = _const_grid(scene_mod, 1.0, n, 0.25, 0.75)  # sigma_t 1
+    m = 40000
+    o = np.tile(np.array([[0.5, -0.25, 0.5]], np.float32), (m, 1))
+    d = np.tile(np.array([[0.0, 1.0, 0.0]], np.float32), (m, 1))
+    t, _ = oracle.grid_eval(s, "sample", o, d, np.full(m, 1.5, np.float32))
+    integral = 1 - 1.0 / n + 2 * (0.5 / n) * 0.75
+    p = float((t < 0).mean())
+    want = np.exp(-integral)
+    assert abs(p - want) < 4 * np.sqrt(want * (1 - want) / m)
+    hit = t[t >= 0]
+    assert np.all((hit >= 0.25 - 1e-5) & (hit <= 1.25 + 1e-5))  # medium-space t inside the cube
+
+
+def test_grid_ray_transform_and_miss(oracle, scene_mod):
+    """WorldToMedium maps world to medium space (a scaled + translated grid), and rays that miss
+    the medium box use no draws and give Tr = 1 (grid.cpp:68-70, 96-98)."""
+    s = _const_grid(scene_mod, 1.0, 4)
+    # grid over world [2, 4]^3: world_to_medium = Scale(1/2) * Translate(-2)
+    w2m = np.array([[0.5, 0, 0, -1], [0, 0.5, 0, -1], [0, 0, 0.5, -1], [0, 0, 0, 1]], np.float32)
+    s = scene_mod.grid_medium(s, np.full(64, 1.0, np.float32), 4, w2m)
+    tr, draws = oracle.grid_eval(s, "tr", np.array([[0.5, 0.5, 0.5]], np.float32), np.array([[1, 0, 0]], np.float32),
+                                 np.array([1.0], np.float32))
+    assert tr.tolist() == [1.0] and draws.tolist() == [0]
+    m = 20000
+    o = np.tile(np.array([[1.0, 3.0, 3.0]], np.float32), (m, 1))
+    d = np.tile(np.array([[1.0, 0.0, 0.0]], np.float32), (m, 1))
+    tr, _ = oracle.grid_eval(s, "tr", o, d, np.full(m, 4.0, np.float32))
+    # the tracking parameter t is world distance (the world direction is normalised before the
+    # transform, grid.cpp:66-67) while Density is looked up in medium space: the crossing is 2
+    # world units of the same density profile as above (n = 4), so the optical depth doubles
+    integral = 1 - 1.0 / 4 + 2 * (0.5 / 4) * 0.75
+    want = np.exp(-2.0 * 2.0 * integral)
+    assert abs(tr.mean() - want) < 4 * tr.std() / np.sqrt(m) + 1e-4
+
+
+@pytest.mark.parametrize("depth,it", [(5, 0), (6, 2)])
+def test_oracle_matches_python_restatement_grid(oracle, scene_mod, depth, it):
+    """The C++ oracle's GridDensityMedium photon paths (delta + ratio tracking draws) agree bit for
+    bit with the independent Python restatement."""
+    s = scene_mod.cornell_smoke_scene(n=16)
+    n, k = 3000, 60
+    ref = oracle.trace_photons(s, n, iteration=it, max_depth=depth)
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        py = rp.trace_photons(s, n, iteration=it, max_depth=depth, first=k)
+    assert np.array_equal(ref["counts"][:k], py["counts"])
+    nb = int(py["counts"].sum())
+    for key in ("start", "end", "radius", "power"):
+        assert np.array_equal(ref[key][:nb].view(np.uint32), py[key].view(np.uint32)), key
+
+
+def test_smoke_scene_struct_matches_library(bre, scene_mod):
+    lib = bre.load_library()
+    s = scene_mod.Scene()
+    dens = scene_mod.smoke_density(8, 7)
+    lib.bre_scene_cornell_smoke(ctypes.addressof(s), ctypes.c_float(0.5), ctypes.c_float(4.5), ctypes.c_float(0.7),
+                                8, dens.ctypes.data_as(ctypes.c_void_p))
+    want = scene_mod.cornell_smoke_scene(0.5, 4.5, 0.7, n=8, density=dens)
+    assert s.to_bytes() == want.to_bytes()
+    d2 = scene_mod.smoke_density(8, 7)
+    assert np.array_equal(dens, d2) and dens.min() >= 0 and dens.max() > 0.5
