@@ -24,6 +24,7 @@ STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
 OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
+OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS = 11, 12, 13
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -54,7 +55,7 @@ class Stats(ctypes.Structure):
                 ("n_photons", ctypes.c_int64),
                 ("photon_ms", ctypes.c_double),
                 ("n_camera_segments", ctypes.c_int64),
-                ("camera_ms", ctypes.c_double)]
+                ("camera_ms", ctypes.c_double), ("n_chunks", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -56,17 +56,27 @@ struct bre_ctx {
     int kernel = 0;
     int leaf_size = 1;
     int sqrt_mode = 0;
-    int split = 16;
+    int split = 8;
     bool prefilter = true;
     int debug_mode = 0;
     int stack_limit = 0;
     int occupancy = 0;
+    float loose_cos = 0.f;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 32;          // auto mode: leaf size of the tile tree kernel 4 takes hand-overs on
     int built_leaf2 = 0;     // 0: no tile tree for the current beam set
     int roots2_split = -1;
     DevMem nodes2, roots2;
+    // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
+    int chunk_len = 400;   // chunk length in units of E / 100
+    int chunk_leaf = 1;    // chunks per LBVH leaf
+    DevMem ch_bounds, ch_counts, ch_offsets, ch_range, ch_scan_tmp, ch_box, ch_cent, ch_slo, ch_shi, ch_par,
+        ch_recs, ch_cpar, ch_nodes;
+    int64_t n_chunks = 0;
+    // coherence sort of the camera-pass segments before the gather (bre_sort.hip)
+    bool sort_segments = true;
+    DevMem ss_bounds, ss_keys, ss_keys_alt, ss_vals, ss_vals_alt, ss_tmp, ss_o, ss_p, ss_d, ss_t, ss_pix;
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     int built_leaf_size = 1;
@@ -211,6 +221,117 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     return BRE_OK;
 }
 
+bre_status read_counters(bre_ctx *c, DevCounters *ctr);
+
+// Kernel 5: build the capsule-chunk index for this gather's segments and R, then gather through it
+// (bre_chunk.hip).  Every array is a context buffer reused across calls; the beam build's sort
+// scratch (keys / vals / sort_tmp / leaf_parent / visit) is reused, it is dead after the build.
+bre_status gather_chunk(bre_ctx *c, const GatherArgs &a) {
+    const int64_t np = c->nvalid;
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    ChunkBuild cb;
+    HIPCHK(c, c->ch_bounds.ensure(12 * sizeof(unsigned int)));
+    HIPCHK(c, c->ch_counts.ensure((size_t)(np + 1) * sizeof(int32_t)));
+    HIPCHK(c, c->ch_offsets.ensure((size_t)(np + 1) * sizeof(int64_t)));
+    HIPCHK(c, c->ch_range.ensure((size_t)(2 * np + 2) * sizeof(float)));
+    const size_t st = chunk_scan_temp_bytes(np);
+    HIPCHK(c, c->ch_scan_tmp.ensure(st + 16));
+    cb.parents = c->recs.as<BeamRec>();
+    cb.nparents = np;
+    cb.seg_o = a.o;
+    cb.seg_p = a.p;
+    cb.nseg = a.nseg;
+    cb.R = a.R;
+    cb.len_factor = (float)c->chunk_len / 100.f;
+    cb.seg_bounds = c->ch_bounds.as<unsigned int>();
+    cb.cbounds = c->ch_bounds.as<unsigned int>() + 6;
+    cb.counts = c->ch_counts.as<int32_t>();
+    cb.offsets = c->ch_offsets.as<int64_t>();
+    cb.range = c->ch_range.as<float>();
+    cb.scan_tmp = c->ch_scan_tmp.ptr;
+    cb.scan_tmp_bytes = st;
+    HIPCHK(c, launch_chunk_count(cb, c->stream));
+    int64_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, cb.offsets + np, sizeof(total), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (total > ((int64_t)1 << 30))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: kernel 5 needs %lld chunks (> 2^30); raise BRE_OPT_CHUNK_LEN "
+                    "or use kernel 0", (long long)total);
+    c->n_chunks = total;
+    if (total == 0) {
+        HIPCHK(c, launch_zero_outputs(a, c->stream));
+        return BRE_OK;
+    }
+    const size_t C = (size_t)total;
+    const int K = c->chunk_leaf;
+    const int64_t nleaf = (total + K - 1) / K;
+    const int64_t nnodes = nleaf > 1 ? nleaf - 1 : 1;
+    HIPCHK(c, c->ch_box.ensure(C * 6 * sizeof(float)));
+    HIPCHK(c, c->ch_cent.ensure(C * 3 * sizeof(float)));
+    HIPCHK(c, c->ch_slo.ensure(C * sizeof(float)));
+    HIPCHK(c, c->ch_shi.ensure(C * sizeof(float)));
+    HIPCHK(c, c->ch_par.ensure(C * sizeof(int32_t)));
+    HIPCHK(c, c->keys.ensure(C * sizeof(unsigned long long)));
+    HIPCHK(c, c->keys_alt.ensure(C * sizeof(unsigned long long)));
+    HIPCHK(c, c->vals.ensure(C * sizeof(int32_t)));
+    HIPCHK(c, c->vals_alt.ensure(C * sizeof(int32_t)));
+    const size_t sb = sort_temp_bytes(total);
+    HIPCHK(c, c->sort_tmp.ensure(sb + 16));
+    HIPCHK(c, c->ch_recs.ensure(C * sizeof(ChunkRec)));
+    HIPCHK(c, c->ch_cpar.ensure(C * sizeof(int32_t)));
+    HIPCHK(c, c->ch_nodes.ensure((size_t)nnodes * sizeof(Node)));
+    HIPCHK(c, c->leaf_parent.ensure((size_t)nleaf * sizeof(int32_t)));
+    HIPCHK(c, c->visit.ensure((size_t)nnodes * sizeof(unsigned int)));
+    HIPCHK(c, launch_chunk_emit(cb, c->ch_box.as<float>(), c->ch_cent.as<float>(), c->ch_slo.as<float>(),
+                                c->ch_shi.as<float>(), c->ch_par.as<int32_t>(), c->stream));
+    BuildBuffers bb{};
+    bb.n = total;
+    bb.leaf_size = K;
+    bb.box = c->ch_box.as<float>();
+    bb.cent = c->ch_cent.as<float>();
+    bb.cbounds = cb.cbounds;
+    bb.keys = c->keys.as<unsigned long long>();
+    bb.keys_alt = c->keys_alt.as<unsigned long long>();
+    bb.vals = c->vals.as<int32_t>();
+    bb.vals_alt = c->vals_alt.as<int32_t>();
+    bb.sort_tmp = c->sort_tmp.ptr;
+    bb.sort_tmp_bytes = sb;
+    bb.leaf_parent = c->leaf_parent.as<int32_t>();
+    bb.visit = c->visit.as<unsigned int>();
+    bb.recs = reinterpret_cast<BeamRec *>(c->ch_recs.as<ChunkRec>());  // same leading lo / hi layout
+    bb.nodes = c->ch_nodes.as<Node>();
+    HIPCHK(c, launch_morton(bb, c->stream));
+    HIPCHK(c, launch_sort(bb, c->stream));
+    HIPCHK(c, launch_chunk_pack(cb, total, bb.vals_alt, bb.box, c->ch_slo.as<float>(), c->ch_shi.as<float>(),
+                                c->ch_par.as<int32_t>(), c->ch_recs.as<ChunkRec>(), c->ch_cpar.as<int32_t>(),
+                                c->stream));
+    HIPCHK(c, launch_hierarchy(bb, total, c->stream));
+    ChunkGatherArgs g;
+    g.nseg = a.nseg;
+    g.o = a.o;
+    g.p = a.p;
+    g.d = a.d;
+    g.tmax = a.tmax;
+    g.pixel = a.pixel;
+    g.R = a.R;
+    g.npix = a.npix;
+    g.accum = a.accum;
+    g.seg_rgb = a.seg_rgb;
+    g.seg_counts = a.seg_counts;
+    g.chunks = c->ch_recs.as<ChunkRec>();
+    g.chunk_parent = c->ch_cpar.as<int32_t>();
+    g.parents = c->recs.as<BeamRec>();
+    g.pow = c->pow.as<float4>();
+    g.nodes = c->ch_nodes.as<Node>();
+    g.nchunks = total;
+    g.leaf_size = K;
+    g.prefilter = c->prefilter;
+    g.ctr = a.ctr;
+    HIPCHK(c, launch_gather_chunk(g, c->counters, c->stream));
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+    return read_counters(c, a.ctr);
+}
+
 bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
                          const int32_t *pixel, float R, int64_t npix, float *accum, float *seg_rgb,
                          int32_t *seg_counts) {
@@ -246,6 +367,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.debug_mode = c->debug_mode;
     a.stack_limit = c->stack_limit;
     a.occupancy = c->occupancy;
+    a.loose_cos = c->loose_cos;
     a.roots = nullptr;
     a.partial = nullptr;
     a.pcnt = nullptr;
@@ -264,6 +386,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     // auto (0): kernel 3 on the small-leaf tree with kernel 4 on the tile tree taking the packets it
     // hands over; with leaf clusters too large for kernel 3, kernel 4 alone
     int kernel = c->kernel;
+    if (kernel == 5) return gather_chunk(c, a);
     if (kernel == 0 && c->built_leaf2 == 0) kernel = c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 4;
     if (kernel == 3 && c->built_leaf_size > kProxyMaxLeafHost)
         return fail(c, BRE_ERR_STATE, "kernel 3 needs BRE_OPT_LEAF_SIZE <= %d", kProxyMaxLeafHost);
@@ -295,6 +418,10 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+    return read_counters(c, a.ctr);
+}
+
+bre_status read_counters(bre_ctx *c, DevCounters *ctr) {
     if (c->timing || c->counters) {
         DevCounters h;
         HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -314,6 +441,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
         c->stats.max_stack_depth = (int64_t)h.max_stack;
         c->stats.redo_items = (int64_t)h.redo_items;
+        c->stats.n_chunks = c->n_chunks;
         if (h.flags & 1u) return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than stack)");
         if (h.flags & 2u) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix)");
     }
@@ -367,7 +495,11 @@ void bre_destroy(bre_ctx *c) {
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
-                     &c->seg_depth};
+                     &c->seg_depth, &c->grid_dens, &c->nodes2, &c->roots2, &c->ch_bounds, &c->ch_counts,
+                     &c->ch_offsets, &c->ch_range, &c->ch_scan_tmp, &c->ch_box, &c->ch_cent, &c->ch_slo, &c->ch_shi,
+                     &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
+                     &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
+                     &c->ss_t, &c->ss_pix};
     for (DevMem *m : all) m->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -383,7 +515,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
     case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
     case BRE_OPT_KERNEL:
-        if (value < 0 || value > 4) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..4");
+        if (value < 0 || value > 5) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..5");
         c->kernel = (int)value;
         return BRE_OK;
     case BRE_OPT_LEAF_SIZE:
@@ -400,6 +532,16 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->split = (int)value;
         return BRE_OK;
     case BRE_OPT_PREFILTER: c->prefilter = value != 0; return BRE_OK;
+    case BRE_OPT_CHUNK_LEN:
+        if (value < 25 || value > 100000)
+            return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_CHUNK_LEN must be in 25..100000 (units of E/100)");
+        c->chunk_len = (int)value;
+        return BRE_OK;
+    case BRE_OPT_SORT_SEGMENTS: c->sort_segments = value != 0; return BRE_OK;
+    case BRE_OPT_CHUNK_LEAF:
+        if (value < 1 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_CHUNK_LEAF must be in 1..64");
+        c->chunk_leaf = (int)value;
+        return BRE_OK;
     case BRE_OPT_TILE_LEAF:
         if (value < 1 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_TILE_LEAF must be in 1..64");
         c->leaf2 = (int)value;
@@ -417,6 +559,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
     case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
     case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 3 register budget
+    case 103: c->loose_cos = (float)value * 1e-4f; return BRE_OK;  // internal: kernel 3 coherence cut (1e-4)
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
 }
@@ -710,8 +853,32 @@ bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
     if (c->cam_npix == 0) return fail(c, BRE_ERR_STATE, "bre_gather_camera: no camera pass yet");
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
-    return gather_device(c, c->cam_nseg, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
-                         c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, nullptr, nullptr);
+    const int64_t n = c->cam_nseg;
+    if (!c->sort_segments || n < 2)
+        return gather_device(c, n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
+                             c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, nullptr, nullptr);
+    // the segments only add into their pixels here, so the packet kernels may take them in a
+    // coherence order (bre_sort.hip)
+    const size_t N = (size_t)n;
+    HIPCHK(c, c->ss_bounds.ensure(8 * sizeof(unsigned int)));
+    HIPCHK(c, c->ss_keys.ensure(N * sizeof(unsigned long long)));
+    HIPCHK(c, c->ss_keys_alt.ensure(N * sizeof(unsigned long long)));
+    HIPCHK(c, c->ss_vals.ensure(N * sizeof(int32_t)));
+    HIPCHK(c, c->ss_vals_alt.ensure(N * sizeof(int32_t)));
+    const size_t tb = seg_sort_temp_bytes(n);
+    HIPCHK(c, c->ss_tmp.ensure(tb + 16));
+    HIPCHK(c, c->ss_o.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->ss_p.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->ss_d.ensure(N * 3 * sizeof(float)));
+    HIPCHK(c, c->ss_t.ensure(N * sizeof(float)));
+    HIPCHK(c, c->ss_pix.ensure(N * sizeof(int32_t)));
+    SegSort ss{n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(), c->seg_t.as<float>(),
+               c->seg_pix.as<int32_t>(), c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
+               c->ss_keys_alt.as<unsigned long long>(), c->ss_vals.as<int32_t>(), c->ss_vals_alt.as<int32_t>(),
+               c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
+               c->ss_t.as<float>(), c->ss_pix.as<int32_t>()};
+    HIPCHK(c, launch_sort_segments(ss, c->stream));
+    return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, nullptr, nullptr);
 }
 
 bre_status bre_get_segments(bre_ctx *c, int64_t capacity, float *o, float *p, float *d, float *tmax, int32_t *pixel,

@@ -75,6 +75,19 @@ struct BuildBuffers {
     Node *nodes;        // max(nleaf-1, 1)
 };
 
+// One capsule chunk of a beam LINE (kernel 5, bre_chunk.hip): 64 B, same leading lo/hi as
+// BeamRec so the LBVH kernels (k_morton / k_karras / k_refit) build over chunks unchanged.
+struct alignas(16) ChunkRec {
+    float lo[3], hi[3];  // conservative box: the chunk's line piece expanded by E = (R + r)(1+1e-3)+margin
+    float b0[3];         // parent beam start   (ComputeClosestPoints inputs, exactly the parent's)
+    float bu[3];         // parent unit direction
+    float mag_b;         // parent |end - start|
+    float radius;        // parent radius
+    float s_lo, s_hi;    // ownership: the pair belongs to this chunk iff s_lo <= s < s_hi, s = the
+                         // line parameter of ComputeClosestPoints' beam point
+};
+static_assert(sizeof(ChunkRec) == 64, "ChunkRec must be one 64-B line");
+
 // build kernels (bre_build.hip)
 hipError_t launch_prep(const BuildBuffers &b, hipStream_t s);
 hipError_t launch_morton(const BuildBuffers &b, hipStream_t s);
@@ -112,7 +125,71 @@ struct GatherArgs {
     const Node *nodes2;
     const int32_t *roots2;
     int leaf2;
+    float loose_cos;       // kernel 3: packets whose lanes' directions spread wider than this cosine
+                           // are handed over (0: default)
 };
+
+// capsule-chunk index (bre_chunk.hip)
+struct ChunkBuild {
+    const BeamRec *parents;   // sorted parent beam records (reference group boxes)
+    int64_t nparents;
+    const float *seg_o, *seg_p;  // the gather's segments (clip box)
+    int64_t nseg;
+    float R;
+    float len_factor;         // chunk length = len_factor * E
+    unsigned int *seg_bounds;  // 6 ordered uints (scratch)
+    unsigned int *cbounds;     // 6 ordered uints (scratch)
+    int32_t *counts;           // nparents + 1
+    int64_t *offsets;          // nparents + 1
+    float *range;              // 2 * nparents
+    void *scan_tmp;
+    size_t scan_tmp_bytes;
+};
+size_t chunk_scan_temp_bytes(int64_t n);
+// pass 1: clip every parent's line to the segments' box, count its chunks; *total after the scan
+hipError_t launch_chunk_count(const ChunkBuild &c, hipStream_t s);
+// pass 2: emit chunk boxes / centroids (input order) + temp fields
+hipError_t launch_chunk_emit(const ChunkBuild &c, float *box, float *cent, float *s_lo, float *s_hi,
+                             int32_t *parent, hipStream_t s);
+// pass 3 (after morton + sort): sorted ChunkRecs + their parent indices
+hipError_t launch_chunk_pack(const ChunkBuild &c, int64_t nchunks, const int32_t *order, const float *box,
+                             const float *s_lo, const float *s_hi, const int32_t *parent, ChunkRec *out,
+                             int32_t *out_parent, hipStream_t s);
+struct ChunkGatherArgs {
+    int64_t nseg;
+    const float *o, *p, *d, *tmax;
+    const int32_t *pixel;
+    float R;
+    int64_t npix;
+    float *accum, *seg_rgb;
+    int32_t *seg_counts;
+    const ChunkRec *chunks;
+    const int32_t *chunk_parent;
+    const BeamRec *parents;
+    const float4 *pow;
+    const Node *nodes;
+    int64_t nchunks;
+    int leaf_size;
+    bool prefilter;
+    DevCounters *ctr;
+};
+hipError_t launch_gather_chunk(const ChunkGatherArgs &a, bool counters, hipStream_t s);
+
+// coherence sort of a gather's segments (bre_sort.hip): 5-D Morton of (origin, direction)
+struct SegSort {
+    int64_t n;
+    const float *o, *p, *d, *t;
+    const int32_t *pix;
+    unsigned int *bounds;  // 6
+    unsigned long long *keys, *keys_alt;
+    int32_t *vals, *vals_alt;
+    void *tmp;
+    size_t tmp_bytes;
+    float *o2, *p2, *d2, *t2;  // sorted copies
+    int32_t *pix2;
+};
+size_t seg_sort_temp_bytes(int64_t n);
+hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);
 
 // gather kernels (bre_gather.hip)
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);

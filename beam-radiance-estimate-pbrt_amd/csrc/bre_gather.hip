@@ -19,6 +19,7 @@
 #include <float.h>
 
 #include "bre_device.h"
+#include "bre_lane.h"
 #include "bre_math.h"
 
 namespace bre {
@@ -28,128 +29,6 @@ namespace {
 constexpr int kWaveBlock = 256;    // 4 waves
 constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 
-
-// Whole-record loads (4 x 16 B).  With a wave-uniform index these become SMEM loads into SGPRs.
-struct NodeV {
-    Box6 b0, b1;
-    int32_t c0, c1;
-};
-__device__ __forceinline__ NodeV load_node(const Node *__restrict__ nodes, int i) {
-    const float4 *q = reinterpret_cast<const float4 *>(nodes + i);
-    const float4 x = q[0], y = q[1], z = q[2], w = q[3];
-    NodeV n;
-    // Node layout: lo[0] (0-2), lo[1] (3-5), hi[0] (6-8), hi[1] (9-11), child[0], child[1], ...
-    n.b0 = Box6{x.x, x.y, x.z, y.z, y.w, z.x};
-    n.b1 = Box6{x.w, y.x, y.y, z.y, z.z, z.w};
-    n.c0 = __float_as_int(w.x);
-    n.c1 = __float_as_int(w.y);
-    return n;
-}
-struct BeamV {
-    Box6 box;
-    f3 b0, bu;
-    float mag_b, radius;
-    f3 pw;  // scaled powerEnd, when the caller already has it (kernel 3 batches)
-};
-__device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int64_t i) {
-    const float4 *q = reinterpret_cast<const float4 *>(recs + i);
-    const float4 x = q[0], y = q[1], z = q[2], w = q[3];
-    BeamV r;
-    r.box = Box6{x.x, x.y, x.z, x.w, y.x, y.y};
-    r.b0 = mk(y.z, y.w, z.x);
-    r.bu = mk(z.y, z.z, z.w);
-    r.mag_b = w.x;
-    r.radius = w.y;
-    r.pw = mk(0.f, 0.f, 0.f);
-    return r;
-}
-
-struct Lane {
-    f3 o, p, au, d;
-    f3 inv, invs;
-    float tmax, mag_a;
-    float omax;  // max |o_i| + |A|: bounds the segment-side coordinates (prefilter margin)
-    int n0, n1, n2;
-    bool has_inf;  // some 1/d_i is infinite (invs != inv)
-};
-
-__device__ __forceinline__ float sanitize_inv(float v) {
-    return isinf(v) ? copysignf(FLT_MAX, v) : v;
-}
-
-__device__ __forceinline__ bool load_lane(int64_t s, int64_t nseg, const float *__restrict__ o,
-                                          const float *__restrict__ p, const float *__restrict__ d,
-                                          const float *__restrict__ tmax, Lane &L) {
-    if (s >= nseg) {
-        L.o = L.p = L.au = L.d = L.inv = L.invs = mk(0.f, 0.f, 0.f);
-        L.tmax = 0.f;
-        L.mag_a = 0.f;
-        L.omax = 0.f;
-        L.n0 = L.n1 = L.n2 = 0;
-        L.has_inf = false;
-        return false;
-    }
-    L.o = mk(o[3 * s], o[3 * s + 1], o[3 * s + 2]);
-    L.p = mk(p[3 * s], p[3 * s + 1], p[3 * s + 2]);
-    const f3 dd = mk(d[3 * s], d[3 * s + 1], d[3 * s + 2]);
-    L.d = dd;
-    L.tmax = tmax[s];
-    // invDir(1 / ray.d.x, ...), dirIsNeg = invDir < 0  (photonbeambvh.cpp:690-691)
-    L.inv = mk(1 / dd.x, 1 / dd.y, 1 / dd.z);
-    L.invs = mk(sanitize_inv(L.inv.x), sanitize_inv(L.inv.y), sanitize_inv(L.inv.z));
-    L.has_inf = isinf(L.inv.x) || isinf(L.inv.y) || isinf(L.inv.z);
-    L.n0 = L.inv.x < 0;
-    L.n1 = L.inv.y < 0;
-    L.n2 = L.inv.z < 0;
-    // A = a1 - a0; magA = |A|; A /= magA   (photonbeam.cpp:90-92, 121)
-    const f3 A = sub3(L.p, L.o);
-    L.mag_a = len3(A);
-    L.au = (L.mag_a != 0.0f) ? div3(A, L.mag_a) : mk(0.f, 0.f, 0.f);
-    L.omax = fmaxf(fmaxf(fabsf(L.o.x), fabsf(L.o.y)), fabsf(L.o.z)) + L.mag_a;
-    return true;
-}
-
-// Conservative reject ahead of the exact closest-point code.  Every point the reference's
-// ComputeClosestPoints returns lies (to within a few ulps of the largest coordinate involved) on the
-// line a0 + s*au or b0 + t*bu, so its distance is at least the line-line distance
-// |t.(au x bu)| / |au x bu| minus that rounding.  With |au x bu|^2 >= 1e-2 the beam-side parameter is
-// bounded (|t1| <= |t|/|au x bu| <= 10|t|), so the coordinates, and the rounding, are bounded too;
-// nearer-parallel pairs always take the exact path.  A pair rejected here cannot have a computed
-// distance below R + r, so skipping it changes no result bit (the parity tests count every pair).
-__device__ __forceinline__ bool far_from_lines(const Lane &L, const BeamV &r, float maxd) {
-    if (L.mag_a == 0.0f) return false;
-    const f3 t = sub3(r.b0, L.o);
-    const f3 n = mk(L.au.y * r.bu.z - L.au.z * r.bu.y, L.au.z * r.bu.x - L.au.x * r.bu.z,
-                    L.au.x * r.bu.y - L.au.y * r.bu.x);
-    const float nn = lensq3(n);
-    if (!(nn >= 1e-2f)) return false;
-    const float tn = fabsf(dot3(t, n));
-    const float tl = fabsf(t.x) + fabsf(t.y) + fabsf(t.z);
-    const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
-    const float mag = L.omax + bmax + 10.0f * tl;       // bound on every coordinate involved
-    const float eps = 1e-5f * mag + 1e-6f;               // >> the few-ulp rounding of those points
-    const float nl = __builtin_sqrtf(nn);
-    return (tn - 1e-6f * tl) > (maxd * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
-}
-
-// far_from_lines with FMAs and the hardware sqrt: the same bound, evaluated to within a few ulps
-// of the exact values, far inside its margins (1e-6 relative on |t.n|, |n| and the 1e-5 eps).
-// Any rejection is still a proof that the reference's computed distance is >= maxd.
-__device__ __forceinline__ bool far_from_lines_fast(f3 o, f3 au, float mag_a, float omax, f3 b0, f3 bu, float maxd) {
-    if (mag_a == 0.0f) return false;
-    const f3 t = sub3(b0, o);
-    const f3 n = mk(__builtin_fmaf(au.y, bu.z, -(au.z * bu.y)), __builtin_fmaf(au.z, bu.x, -(au.x * bu.z)),
-                    __builtin_fmaf(au.x, bu.y, -(au.y * bu.x)));
-    const float nn = __builtin_fmaf(n.x, n.x, __builtin_fmaf(n.y, n.y, n.z * n.z));
-    if (!(nn >= 1e-2f)) return false;
-    const float tn = fabsf(__builtin_fmaf(t.x, n.x, __builtin_fmaf(t.y, n.y, t.z * n.z)));
-    const float tl = fabsf(t.x) + fabsf(t.y) + fabsf(t.z);
-    const float bmax = fmaxf(fmaxf(fabsf(b0.x), fabsf(b0.y)), fabsf(b0.z));
-    const float mag = omax + bmax + 10.0f * tl;
-    const float eps = 1e-5f * mag + 1e-6f;
-    const float nl = __builtin_amdgcn_sqrtf(nn) * 1.000001f;  // v_sqrt_f32 (1 ulp) rounded up
-    return (tn - 1e-6f * tl) > (maxd * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
-}
 
 // Evaluate one beam record for one lane: reference box test, closest points, kernel.
 struct Prof {
@@ -448,7 +327,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_gather_wave(
 // the proxy computes with the same float operations, because rounding is monotone and the
 // function is bilinear).  The proxy only decides WHICH beams get the exact per-lane test.
 constexpr int kProxyStack = 1024;  // LDS node-stack entries per wave (>= kStackDepth: reused by dfs); 550 seen at C2
-constexpr float kLooseCos = 0.9976f;  // packets whose directions spread > ~4 deg use the dfs path
+constexpr float kLooseCos = 0.9976f;  // default: packets whose directions spread > ~4 deg use the dfs path
 constexpr int kProxyMaxLeaf = 4;             // kernel 3 needs leaf clusters of <= 4 beams
 constexpr int kCandCap = 64 + 2 * 64 * kProxyMaxLeaf;  // leftover + one step's leaf beams
 
@@ -562,15 +441,132 @@ __device__ __forceinline__ void proxy_batch(const Lane &L, bool valid, const int
     }
 }
 
+// Compacted form of proxy_batch (the default).  The batch's beam lines and powers are staged in
+// LDS once (one 64-B line + 16 B per lane).  Per lane and beam only the conservative line-distance
+// prefilter runs (beam line broadcast from LDS); the (beam, lane) pairs it keeps (~1 in 8 at C2)
+// go to a ring in LDS, and every 64 of them (and the batch's remainder) run the reference's box
+// test on the beam's group box, ComputeClosestPoints and the kernel with all lanes busy, one pair
+// per lane, beam data read back from the staged lines, adding into the segment's LDS accumulator.
+// The contributing pairs are the same (a contribution needs both the box hit and d < R + r; the
+// prefilter only drops pairs with d >= R + r), each pair's value is computed by the same
+// arithmetic, and a segment's pairs are summed in candidate-list order as in proxy_batch.
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+constexpr int kPQueue = 128;  // >= 63 left over + 64 appended by one beam
+
+struct ProxyQ {
+    float4 bst[64][4];     // staged BeamRec lines of the current batch
+    float4 bpw[64];        // their scaled powers
+    float acc[3][64];      // per-segment RGB
+    int32_t cnt[64];       // per-segment contribution counts (counters only)
+    uint16_t q[kPQueue];   // ring: staged slot | segment lane << 8
+};
+
+// all lanes call; lanes < n take pair (first + lane) of the ring
+template <bool COUNT>
+__device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, int n, float R, Prof &pf) {
+    const int lane = threadIdx.x & 63;
+    const bool on = lane < n;
+    const unsigned qv = q.q[(first + (on ? lane : 0)) & (kPQueue - 1)];
+    const int j = (int)(qv & 0xffu), sl = (int)(qv >> 8);
+    const f3 o = mk(__shfl(M.o.x, sl), __shfl(M.o.y, sl), __shfl(M.o.z, sl));
+    const f3 p = mk(__shfl(M.p.x, sl), __shfl(M.p.y, sl), __shfl(M.p.z, sl));
+    const f3 au = mk(__shfl(M.au.x, sl), __shfl(M.au.y, sl), __shfl(M.au.z, sl));
+    const f3 invs = mk(__shfl(M.invs.x, sl), __shfl(M.invs.y, sl), __shfl(M.invs.z, sl));
+    const float mag_a = __shfl(M.mag_a, sl);
+    const float tmax = __shfl(M.tmax, sl);
+    const bool inf = __shfl((int)M.has_inf, sl) != 0;
+    const float4 x = q.bst[j][0], y = q.bst[j][1], z = q.bst[j][2], w = q.bst[j][3];
+    const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+    if (COUNT && lane == 0) ++pf.ccp_waves;
+    // the reference's candidate test on the beam's (group) box, as eval_beam
+    float te;
+    bool hit = on & node_test(box, o, invs, tmax, te);
+    if (__ballot(on & inf) != 0ull) {
+        if (on & inf) {
+            const f3 d = mk(__shfl(M.d.x, sl), __shfl(M.d.y, sl), __shfl(M.d.z, sl));
+            const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+            hit = slab_test(box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
+        }
+    }
+    if (__ballot(hit) == 0ull) return;
+    if (hit) {
+        const f3 b0 = mk(y.z, y.w, z.x), bu = mk(z.y, z.z, z.w);
+        const float maxd = R + w.y;  // MaxDistance = currentBeamRadius + beam->radius
+        float dist;
+        const bool ok = closest_distance(o, p, au, mag_a, b0, bu, w.x, dist);
+        if (ok & (dist < maxd)) {
+            const float rr = dist / maxd;
+            const float wt = sqrtf(1.0f - rr * rr);
+            const float4 pv = q.bpw[j];
+            atomicAdd(&q.acc[0][sl], pv.x * wt);
+            atomicAdd(&q.acc[1][sl], pv.y * wt);
+            atomicAdd(&q.acc[2][sl], pv.z * wt);
+            if (COUNT) atomicAdd(&q.cnt[sl], 1);
+        }
+    }
+}
+
+template <bool COUNT, bool PREF>
+__device__ __forceinline__ void proxy_batch_q(ProxyQ &q, const Lane &L, bool valid, const int32_t *cand, int nb,
+                                              const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                              float R, int &ccount, Prof &pf, int dbg) {
+    const int lane = threadIdx.x & 63;
+    if (lane < nb) {
+        const int32_t bi = cand[lane];
+        const float4 *src = reinterpret_cast<const float4 *>(recs + bi);
+        const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = pw[bi];
+        q.bst[lane][0] = a;
+        q.bst[lane][1] = b;
+        q.bst[lane][2] = c;
+        q.bst[lane][3] = d;
+        q.bpw[lane] = e;
+    }
+    if (COUNT) pf.beams += nb;
+    __builtin_amdgcn_wave_barrier();
+    int qh = 0, qt = 0;  // wave-uniform ring head / tail (the ring is drained per batch)
+    for (int j = 0; j < nb; ++j) {
+        const float4 y = q.bst[j][1], z = q.bst[j][2], w = q.bst[j][3];
+        const f3 b0 = mk(y.z, y.w, z.x), bu = mk(z.y, z.z, z.w);
+        bool need = valid;
+        if (PREF) need = valid && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, b0, bu, R + w.y);
+        if (COUNT) {
+            // the reference's candidate count C (box hits), for the parity tests
+            const float4 x = q.bst[j][0];
+            const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+            float te;
+            bool hit = valid & node_test(box, L.o, L.invs, L.tmax, te);
+            if (L.has_inf) hit = valid & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
+            ccount += hit;
+            pf.rejects += hit & !need;
+        }
+        const unsigned long long m = __ballot(need);
+        if (m == 0ull) continue;
+        if (need) q.q[(qt + lanes_below(m)) & (kPQueue - 1)] = (uint16_t)(j | (lane << 8));
+        qt += __popcll(m);
+        __builtin_amdgcn_wave_barrier();
+        if (qt - qh >= 64) {
+            if (dbg != 2) pq_exact<COUNT>(q, L, qh, 64, R, pf);
+            qh += 64;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (qt > qh && dbg != 2) pq_exact<COUNT>(q, L, qh, qt - qh, R, pf);
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool COUNT, bool PREF, int MINW>
 __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
     const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
     int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int stack_limit, int dbg,
-    uint8_t *__restrict__ redo) {
+    uint8_t *__restrict__ redo, float loose_cos) {
     __shared__ int32_t stk[kProxyStack];
     __shared__ int32_t cand[kCandCap];
+    __shared__ ProxyQ pq;
     int sub;
     int64_t grp;
     if (S >= 8) {
@@ -593,6 +589,10 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
     unsigned long long tests = 0;
     int maxsp = 0;
     bool overflow = false;
+    pq.acc[0][lane] = 0.f;
+    pq.acc[1][lane] = 0.f;
+    pq.acc[2][lane] = 0.f;
+    pq.cnt[lane] = 0;
 
     // Incoherent packets (directions spread wider than kLooseCos) make the proxy useless: they take
     // the depth-first per-lane path instead (kernel 1's traversal, same exact per-lane tests).
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
         const float sn = sqrtf(sx * sx + sy * sy + sz * sz);
         const float dn = sqrtf(lensq3(L.d));
         const float c = (valid && sn > 0.f && dn > 0.f) ? (sx * L.d.x + sy * L.d.y + sz * L.d.z) / (sn * dn) : 1.0f;
-        loose = wave_min(c) < kLooseCos;
+        loose = wave_min(c) < loose_cos;
     }
     if (loose) {
         // handed to kernel 1 (depth-first per-lane traversal), which runs behind this launch
@@ -627,8 +627,11 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
         }
         __builtin_amdgcn_wave_barrier();
         while (sp > 0 || nc > 0) {
+            // 1. pop up to 64 nodes and issue their loads ...
+            int n = 0;
+            NodeV nd{};
             if (sp > 0) {
-                int n = min(64, sp);
+                n = min(64, sp);
                 if (sp + n > stack_limit) n = stack_limit - sp;
                 if (n <= 0) {
                     overflow = true;
@@ -639,10 +642,20 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
                 if (lane < n) node = stk[base + lane];
                 __builtin_amdgcn_wave_barrier();
                 sp = base;
+                if (lane < n) nd = load_node(nodes, node);
+            }
+            // 2. ... and evaluate the full candidate batches gathered so far while they are in flight
+            while (nc >= 64) {
+                nc -= 64;
+                if (dbg != 1)  // dbg 1: timing-only traversal
+                    proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, 64, recs, pw, R, ccount, pf, dbg);
+                __builtin_amdgcn_wave_barrier();
+            }
+            // 3. test the popped nodes' children against the packet proxy
+            if (n > 0) {
                 bool h0 = false, h1 = false;
                 int32_t c0 = kEmptyChild, c1 = kEmptyChild;
                 if (lane < n) {
-                    const NodeV nd = load_node(nodes, node);
                     c0 = nd.c0;
                     c1 = nd.c1;
                     h0 = (c0 != kEmptyChild) && proxy_test(P, nd.b0);
@@ -678,16 +691,22 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-            // evaluate full batches (and the remainder once the stack is empty)
-            while (nc >= 64 || (sp == 0 && nc > 0)) {
-                const int nb = min(64, nc);
-                nc -= nb;
-                if (dbg != 1)  // dbg 1: timing-only traversal
-                    proxy_batch<COUNT, PREF>(L, valid, cand + nc, nb, recs, pw, R, cr, cg, cb, ccount, contrib, pf,
-                                             dbg);
-                __builtin_amdgcn_wave_barrier();
+            // 4. the stack is empty: evaluate what is left
+            if (sp == 0) {
+                while (nc > 0) {
+                    const int nb = min(64, nc);
+                    nc -= nb;
+                    if (dbg != 1)
+                        proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, nb, recs, pw, R, ccount, pf, dbg);
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
         }
+        __builtin_amdgcn_wave_barrier();
+        cr = pq.acc[0][lane];
+        cg = pq.acc[1][lane];
+        cb = pq.acc[2][lane];
+        contrib = pq.cnt[lane];
     }
     if (loose || overflow) {
         // kernel 1 redoes this packet for every subtree; nothing of this wave is kept
@@ -765,9 +784,6 @@ struct TileShared {
     int32_t stk[kStackDepth];
 };
 
-__device__ __forceinline__ int lanes_below(unsigned long long m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
 __device__ __forceinline__ float lane_f(float v, int src) { return __shfl(v, src); }
 
 // Stage 3: exact closest points + kernel for n queued pairs (one per lane; all lanes call).
@@ -1228,7 +1244,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     hipLaunchKernelGGL((k_gather_proxy<C, P, W>), grid3, dim3(64), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R,      \
                        a.partial, a.pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots, a.split,       \
                        a.ctr, a.stack_limit > 0 ? min(a.stack_limit, kProxyStack) : kProxyStack, a.debug_mode,    \
-                       a.redo)
+                       a.redo, a.loose_cos > 0.f ? a.loose_cos : kLooseCos)
 #define BRE_LAUNCH_PROXY(C, P) BRE_LAUNCH_PROXY_W(C, P, 1)
         if (counters) {
             if (a.prefilter) BRE_LAUNCH_PROXY(true, true);

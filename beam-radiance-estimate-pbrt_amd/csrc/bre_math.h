@@ -137,13 +137,19 @@ __host__ __device__ __forceinline__ bool node_test(const Box6 &b, f3 o, f3 invs,
 //   beam    B: b0, bu = (b1-b0)*(1/|B|), mag_b = |b1-b0| (> 0: zero-length beams have a NaN
 //              WorldBound and never become candidates, so the magB==0 branch is unreachable)
 // Returns false for parallel lines (no contribution).  Writes |aClosest - bClosest|.
-__host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu, float mag_b,
-                                                          float &dist) {
+// With WANT_S, also returns the beam-line parameter s of the returned beam point, pB = b0 + bu*s
+// (t1 when t0 is inside A, else the clamped projection of A's endpoint): the capsule-chunk
+// index (bre_chunk.hip) assigns each pair to the chunk whose ownership interval holds s.
+template <bool WANT_S>
+__host__ __device__ __forceinline__ bool closest_distance_t(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu,
+                                                            float mag_b, float &dist, float &s_out) {
     if (mag_a == 0.0f) {
         // A is a point: project a0 onto B, clamp (photonbeam.cpp:95-108)
         const float d = dot3(sub3(a0, b0), bu);
-        const f3 bc = add3(b0, scale3(bu, clampf_ref(d, 0.0f, mag_b)));
+        const float dc = clampf_ref(d, 0.0f, mag_b);
+        const f3 bc = add3(b0, scale3(bu, dc));
         dist = len3(sub3(a0, bc));
+        if (WANT_S) s_out = dc;
         return true;
     }
     const f3 cr = cross3d(au, bu);
@@ -156,18 +162,27 @@ __host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, f
     const float t1 = detB / denom;
     f3 pA = add3(a0, scale3(au, t0));
     f3 pB = add3(b0, scale3(bu, t1));
+    float sb = t1;
     if (t0 < 0) pA = a0;
     else if (t0 > mag_a) pA = a1;
     if (t0 < 0 || t0 > mag_a) {
         const float d = clampf_ref(dot3(bu, sub3(pA, b0)), 0.0f, mag_b);
         pB = add3(b0, scale3(bu, d));
+        sb = d;
     }
     if (t1 < 0 || t1 > mag_b) {
         const float d = clampf_ref(dot3(au, sub3(pB, a0)), 0.0f, mag_a);
         pA = add3(a0, scale3(au, d));
     }
     dist = len3(sub3(pA, pB));
+    if (WANT_S) s_out = sb;
     return true;
+}
+
+__host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu, float mag_b,
+                                                          float &dist) {
+    float unused;
+    return closest_distance_t<false>(a0, a1, au, mag_a, b0, bu, mag_b, dist, unused);
 }
 
 }  // namespace bre

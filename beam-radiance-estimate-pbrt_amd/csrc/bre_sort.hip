@@ -1,0 +1,160 @@
+// bre_sort.hip — coherence sort of an iteration's camera segments before the gather.
+//
+// The reference gathers segment by segment inside each camera path (photonbeam.cpp:494-508); the
+// batched gather is order-free (each segment's sum goes to its pixel), so the segments can be
+// handed to the packet kernels in any order.  Camera rays of one 8x8 pixel tile form coherent
+// 64-lane packets, but the bounce segments (depth >= 1) leave the walls in cosine-distributed
+// directions: a packet of 64 unrelated rays visits the union of 64 traversals.  Sorting by a 5-D
+// Morton key of (origin in the segments' box, octahedral direction) puts segments that start
+// close together AND point the same way into the same packet, so the packet kernels share most
+// of their node and beam visits again.  Only the order changes; every per-segment sum and every
+// pixel total is the same set of pair contributions.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <float.h>
+
+#include "bre_device.h"
+#include "bre_math.h"
+
+namespace bre {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ unsigned int f2ord(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ void k_sort_init(unsigned int *b) {
+    if (threadIdx.x < 6) b[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_origin_bounds(int64_t n, const float *__restrict__ o,
+                                                          unsigned int *__restrict__ b) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
+    bool any = false;
+    if (i < n) {
+        const float v[3] = {o[3 * i], o[3 * i + 1], o[3 * i + 2]};
+        if (isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2])) {
+            any = true;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) mn[k] = mx[k] = f2ord(v[k]);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], off));
+            mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
+        }
+    }
+    if ((threadIdx.x & 63) == 0 && __ballot(any) != 0ull) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(&b[k], mn[k]);
+            atomicMax(&b[3 + k], mx[k]);
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned int quant10(float x) {  // x in [0, 1]
+    const float q = fminf(fmaxf(x, 0.f), 1.f) * 1023.f;
+    return (unsigned int)q;
+}
+
+// 5-D Morton key: 10 bits each of origin x, y, z (in the origins' box) and the octahedral
+// direction u, v, interleaved from the most significant bit down
+__global__ __launch_bounds__(kBlock) void k_seg_keys(int64_t n, const float *__restrict__ o,
+                                                     const float *__restrict__ d, const unsigned int *__restrict__ b,
+                                                     unsigned long long *__restrict__ keys,
+                                                     int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float lo[3] = {ord2f(b[0]), ord2f(b[1]), ord2f(b[2])};
+    const float hi[3] = {ord2f(b[3]), ord2f(b[4]), ord2f(b[5])};
+    unsigned int q[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float ext = hi[k] - lo[k];
+        q[k] = quant10(ext > 0.f ? (o[3 * i + k] - lo[k]) / ext : 0.f);
+    }
+    // octahedral map of the direction
+    float dx = d[3 * i], dy = d[3 * i + 1], dz = d[3 * i + 2];
+    const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+    float u = 0.f, v = 0.f;
+    if (l1 > 0.f && isfinite(l1)) {
+        dx /= l1;
+        dy /= l1;
+        dz /= l1;
+        u = dx;
+        v = dy;
+        if (dz < 0.f) {
+            u = (1.f - fabsf(dy)) * (dx >= 0.f ? 1.f : -1.f);
+            v = (1.f - fabsf(dx)) * (dy >= 0.f ? 1.f : -1.f);
+        }
+    }
+    q[3] = quant10(0.5f * u + 0.5f);
+    q[4] = quant10(0.5f * v + 0.5f);
+    unsigned long long key = 0ull;
+#pragma unroll
+    for (int bit = 9; bit >= 0; --bit)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t *__restrict__ order,
+                                                        const float *__restrict__ o, const float *__restrict__ p,
+                                                        const float *__restrict__ d, const float *__restrict__ t,
+                                                        const int32_t *__restrict__ pix, float *__restrict__ o2,
+                                                        float *__restrict__ p2, float *__restrict__ d2,
+                                                        float *__restrict__ t2, int32_t *__restrict__ pix2) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t j = order[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        o2[3 * i + k] = o[3 * j + k];
+        p2[3 * i + k] = p[3 * j + k];
+        d2[3 * i + k] = d[3 * j + k];
+    }
+    t2[i] = t[j];
+    pix2[i] = pix[j];
+}
+
+inline unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+size_t seg_sort_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 50);
+    return bytes;
+}
+
+hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
+    if (s.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sort_init, dim3(1), dim3(64), 0, st, s.bounds);
+    hipLaunchKernelGGL(k_origin_bounds, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
+    hipLaunchKernelGGL(k_seg_keys, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.d, s.bounds, s.keys, s.vals);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t bytes = s.tmp_bytes;
+    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, 50, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
+                       s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);
+    return hipGetLastError();
+}
+
+}  // namespace bre

@@ -47,22 +47,33 @@ VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16, help="timed iterations (c2: 16 = the whole 16-spp render)")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed iterations (default: c2 16 = the whole 16-spp render, c5 10 passes, else 4)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["c2", "synthetic"], default="c2")
-    ap.add_argument("--photons", type=int, default=1_000_000, help="c2: photons per iteration")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "synthetic"], default="c2",
+                    help="BASELINE.json configs[1..4] (SURVEY.md §8d) or the kernel-only synthetic set")
+    ap.add_argument("--photons", type=int, default=None, help="photons per iteration (c2 1M, c3 5M, c4 20M, c5 50M)")
     ap.add_argument("--beams", type=int, default=1_000_000, help="synthetic: beams")
-    ap.add_argument("--width", type=int, default=512)
-    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--width", type=int, default=None, help="film width (c2 512, c3/c5 1024, c4 2048)")
+    ap.add_argument("--height", type=int, default=None, help="film height per GPU (weak) or total (strong)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="weak: a W x (H*N) film, H rows per GPU (default); strong: one W x H film split by "
+                         "16x16 tiles over the N GPUs (c4 default)")
+    ap.add_argument("--grid-n", type=int, default=64, help="c3/c5: smoke density grid resolution")
     ap.add_argument("--radius", type=float, default=0.01, help="initialbeamradius (c2) / R (synthetic)")
     ap.add_argument("--alpha", type=float, default=0.5)
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=1)
-    ap.add_argument("--split", type=int, default=16, help="BVH subtrees per segment packet (kernels 1/3)")
+    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet (kernels 1/3)")
     ap.add_argument("--prefilter", type=int, default=1)
+    ap.add_argument("--chunk-len", type=int, default=400, help="kernel 5: chunk length in units of E/100")
+    ap.add_argument("--chunk-leaf", type=int, default=1, help="kernel 5: chunks per LBVH leaf")
+    ap.add_argument("--sort-segments", type=int, default=1, help="coherence-sort the camera segments (0/1)")
     ap.add_argument("--debug-mode", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--loose-cos", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -71,12 +82,29 @@ def parse():
     ap.add_argument("--profile-summary", default=None,
                     help="rocprofv3 PMC summary (profiles/*/profile_summary.json) for roofline.traffic")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    a = ap.parse_args()
+    preset = WORKLOADS.get(a.workload, WORKLOADS["c2"])
+    for k in ("steps", "photons", "width", "height", "scaling"):
+        if getattr(a, k) is None:
+            setattr(a, k, preset[k])
+    return a
+
+
+# BASELINE.json configs[1..4].  c4/c5 are 8-GPU configurations: at N=1 they run
+# as stated (long) unless --photons / --width / --height scale them down.
+WORKLOADS = {
+    "c2": dict(steps=16, photons=1_000_000, width=512, height=512, scaling="weak", medium="fog", g=0.0),
+    "c3": dict(steps=4, photons=5_000_000, width=1024, height=1024, scaling="weak", medium="smoke", g=0.7),
+    "c4": dict(steps=4, photons=20_000_000, width=2048, height=2048, scaling="strong", medium="fog", g=0.0),
+    "c5": dict(steps=10, photons=50_000_000, width=1024, height=1024, scaling="strong", medium="smoke", g=0.7),
+    "synthetic": dict(steps=10, photons=0, width=512, height=512, scaling="weak", medium="fog", g=0.0),
+}
 
 
 KERNEL_NAMES = {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
                 2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over",
-                4: "leaf tiles + wavefront-compacted pair queue"}
+                4: "leaf tiles + wavefront-compacted pair queue",
+                5: "capsule-chunk index (contributing pairs only)"}
 
 
 def main():
@@ -97,22 +125,30 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    W, H = args.width, args.height * world
+    W, H = args.width, args.height * (world if args.scaling == "weak" else 1)
     frame = dmod.ShardedFrame(W, H, rank, world, device=dev)
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
+    g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
+    if args.kernel == 5:
+        g.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
+        g.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
     if args.debug_mode:
         g.set_option(100, args.debug_mode)
     if args.occupancy:
         g.set_option(102, args.occupancy)
+    if args.loose_cos:
+        g.set_option(103, args.loose_cos)
+    if args.tile_leaf:
+        g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     g.set_stream(stream.cuda_stream)
 
-    if args.workload == "c2":
-        wl = C2Workload(args, bre, g, frame, rank, world)
+    if args.workload != "synthetic":
+        wl = SceneWorkload(args, bre, g, frame, rank, world)
     else:
         wl = SyntheticWorkload(args, bre, g, frame, rank, world, dev)
 
@@ -160,7 +196,8 @@ def main():
     c_mean = st["candidates"] / nseg_d
 
     result = {
-        "metric": "beam-radiance estimates/sec at 1M photons",
+        "metric": ("beam-radiance estimates/sec at 1M photons" if args.workload in ("c2", "synthetic") else
+                   f"beam-radiance estimates/sec at {args.photons / 1e6:g}M photons"),
         "value": value,
         "unit": "estimates/s",
         "n_gpus": world,
@@ -168,7 +205,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "fp32",
         "data": wl.data,
@@ -180,10 +217,12 @@ def main():
         "candidate_pair_tests_per_s": c_mean * value,
         "node_visits_per_wave": st["node_visits"] / waves,
         "leaf_visits_per_wave": st["leaf_visits"] / waves,
+        "beam_evals_per_wave": st["beam_evals"] / waves,
         "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / waves,
         "max_stack_depth": st["max_stack_depth"],
         "redo_items": st["redo_items"],
         "prefilter_rejects_per_estimate": st["prefilter_rejects"] / nseg_d,
+        "chunks": st.get("n_chunks", 0),
     }
     result.update(diag)
 
@@ -240,24 +279,30 @@ def pmc_traffic(path):
     return tot / calls if calls else None
 
 
-class C2Workload:
-    """BASELINE.json configs[1]: Cornell box + homogeneous fog, 1M photons/iteration, 512x512."""
-
-    name = "c2"
+class SceneWorkload:
+    """BASELINE.json configs[1..4] as full renders: c2 Cornell box + homogeneous fog (sigma_a 0.05,
+    sigma_s 0.5, g 0); c3/c5 the same box filled with a 64^3 GridDensityMedium of seeded value-noise
+    smoke (sigma_a 0.5, sigma_s 4.5, g 0.7); c4 the fog at 2048^2 with 20M photons."""
 
     def __init__(self, args, bre, g, frame, rank, world):
         import torch
 
         sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
         self.args, self.bre, self.g, self.frame = args, bre, g, frame
-        self.scene = sc.cornell_scene(0.05, 0.5, 0.0)
+        self.name = args.workload
+        preset = WORKLOADS[args.workload]
+        if preset["medium"] == "smoke":
+            self.scene = sc.cornell_smoke_scene(0.5, 4.5, preset["g"], n=args.grid_n, seed=7)
+        else:
+            self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
         g.set_shard(rank, world)
         self.ld = frame.accum
         self.scratch = torch.zeros_like(self.ld)
         self.world = world
-        self.data = ("synthetic scene (SURVEY.md §8d C2: built-in Cornell box + homogeneous fog; photons and camera "
-                     "paths traced on the GPU)")
+        self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "
+                     f"{'grid-density smoke' if preset['medium'] == 'smoke' else 'homogeneous fog'}; photons and "
+                     "camera paths traced on the GPU)")
         self.last_nseg = 0
 
     def radius(self, it):
@@ -305,16 +350,21 @@ class C2Workload:
         return self.radius(0)
 
     def default_profile(self):
-        return os.path.join(ROOT, "profiles", "r04", "profile_summary.json")
+        if self.name != "c2":
+            return None
+        return os.path.join(ROOT, "profiles", "r05", "profile_summary.json")
 
     def config(self):
         a = self.args
-        return {"workload": "C2: Cornell box + homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0), 1M photons/iteration, "
-                            f"{a.width}x{a.height} per GPU, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
+        med = ("homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)" if WORKLOADS[self.name]["medium"] == "fog" else
+               f"GridDensityMedium smoke {a.grid_n}^3 (sigma_a 0.5, sigma_s 4.5, g 0.7)")
+        film = f"{a.width}x{a.height} per GPU" if a.scaling == "weak" else f"{a.width}x{a.height} split over the GPUs"
+        return {"workload": f"{self.name.upper()}: Cornell box + {med}, {a.photons / 1e6:g}M photons/iteration, "
+                            f"{film}, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
                 "photons_per_iteration": a.photons, "image": [self.W, self.H], "iterations_timed": a.steps,
                 "parallelism": f"image-tiles x{self.world}, photons traced on every rank",
                 "kernel": KERNEL_NAMES[a.kernel], "leaf_size": a.leaf_size, "split": a.split,
-                "prefilter": bool(a.prefilter)}
+                "prefilter": bool(a.prefilter), "sort_segments": bool(a.sort_segments)}
 
 
 class SyntheticWorkload:

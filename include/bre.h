@@ -72,7 +72,7 @@ typedef enum bre_option {
                                 leaf tiles with wavefront-compacted pair queues */
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..64 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
-    BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 16) */
+    BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 8) */
     BRE_OPT_PREFILTER = 7,   /* kernels 1/3: 0/1 conservative line-distance reject before the exact
                                 closest-point code (default 1; results are identical either way) */
     BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles t (the reference's
@@ -80,8 +80,14 @@ typedef enum bre_option {
     BRE_OPT_SHARD_COUNT = 9, /* camera pass: number of image-tile shards (default 1 = all tiles).
                                 Set the count before the rank.  Per-pixel results do not depend on
                                 the sharding, so summing the shards' Ld gives the 1-shard image. */
-    BRE_OPT_TILE_LEAF = 10   /* auto mode: beams per leaf tile of the hand-over tree, 1..64 (default
+    BRE_OPT_TILE_LEAF = 10,  /* auto mode: beams per leaf tile of the hand-over tree, 1..64 (default
                                 32); applies at the next build */
+    BRE_OPT_CHUNK_LEN = 11,  /* kernel 5: chunk length in units of E/100, E = (R + r)(1 + 1e-3) + margin
+                                (25..100000, default 400) */
+    BRE_OPT_CHUNK_LEAF = 12, /* kernel 5: chunks per LBVH leaf, 1..64 (default 1) */
+    BRE_OPT_SORT_SEGMENTS = 13 /* bre_gather_camera: 0/1 hand the camera-pass segments to the gather
+                                  in 5-D Morton order of (origin, direction) (default 1); pixel sums
+                                  are the same pair contributions either way */
 } bre_option;
 
 typedef struct bre_stats {
@@ -108,6 +114,7 @@ typedef struct bre_stats {
     double photon_ms;        /* device time of the last photon pass, both passes (timing only) */
     int64_t n_camera_segments; /* segments of the last bre_camera_pass */
     double camera_ms;        /* device time of the last camera pass incl. compaction (timing only) */
+    int64_t n_chunks;        /* kernel 5: chunks in the index of the last gather */
 } bre_stats;
 
 /* ---- context ---- */

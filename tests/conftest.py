@@ -35,3 +35,8 @@ def bre():
 @pytest.fixture(scope="session")
 def synth():
     return importlib.import_module("beam-radiance-estimate-pbrt_amd.synth")
+
+
+@pytest.fixture(scope="session")
+def scene_mod_gpu():
+    return importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")

@@ -226,3 +226,21 @@ def test_render_iteration_grid_matches_oracle(bre, oracle, scene_mod, torch):
     got = ld.cpu().numpy()
     assert _rel_l2(got, ref) <= 1e-3
     assert got.mean() > 0
+
+
+def test_segment_sort_changes_no_pixel(bre, scene_mod, torch):
+    """BRE_OPT_SORT_SEGMENTS: the coherence order of the gather changes the packet grouping and
+    the float order of pixel atomics only; images agree to 1e-6 relative L2."""
+    s = scene_mod.cornell_scene()
+    w, h = 96, 64
+    p = scene_mod.render_params(w, h, iterations=2, photons=30000, max_depth=5, radius=0.03, alpha=0.5)
+    imgs = []
+    for flag in (0, 1):
+        ld = torch.zeros((w * h, 3), dtype=torch.float32, device="cuda")
+        with bre.BeamGather(0) as g:
+            g.set_option(bre.OPT_SORT_SEGMENTS, flag)
+            g.render_iteration(s, p, 1, ld)
+        torch.cuda.synchronize()
+        imgs.append(ld.cpu().numpy().astype(np.float64))
+    assert _rel_l2(imgs[1], imgs[0]) <= 1e-6
+    assert imgs[0].mean() > 0
