@@ -33,6 +33,7 @@ EXPORTS = [
     "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
     "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell", "bre_scene_cornell_smoke", "bre_smoke_density",
     "bre_camera_pass", "bre_gather_camera", "bre_get_segments", "bre_render_iteration", "bre_render",
+    "bre_render_progressive",
 ]
 
 
@@ -127,6 +128,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_render_iteration.restype = I32
     lib.bre_render.argtypes = [P, P, P, P]
     lib.bre_render.restype = I32
+    lib.bre_render_progressive.argtypes = [P, P, P, I32, P, P]
+    lib.bre_render_progressive.restype = I32
     _LIB = lib
     return lib
 

@@ -927,11 +927,11 @@ bre_status bre_render_iteration(bre_ctx *c, const bre_scene *scene, const bre_re
     return BRE_OK;
 }
 
-bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_params *rp, float *image) {
+bre_status bre_render_progressive(bre_ctx *c, const bre_scene *scene, const bre_render_params *rp,
+                                  int32_t write_frequency, bre_image_fn on_image, void *user) {
     if (!c) return BRE_ERR_INVALID_ARG;
     bre_status st = check_params(c, rp);
     if (st != BRE_OK) return st;
-    if (!image) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null image");
     st = set_device(c);
     if (st != BRE_OK) return st;
     const int64_t npix = (int64_t)rp->width * rp->height;
@@ -940,21 +940,53 @@ bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_param
     st = BRE_OK;
     if (hipMemsetAsync(ld, 0, (size_t)npix * 3 * sizeof(float), c->stream) != hipSuccess)
         st = fail(c, BRE_ERR_HIP, "bre_render: memset failed");
-    for (int it = rp->start_iteration; st == BRE_OK && it < rp->end_iteration; ++it)
+    std::vector<float> h, img;
+    for (int it = rp->start_iteration; st == BRE_OK && it < rp->end_iteration; ++it) {
         st = bre_render_iteration(c, scene, rp, it, ld);
-    if (st == BRE_OK) {
-        std::vector<float> h((size_t)npix * 3);
+        if (st != BRE_OK) break;
+        // photonbeam.cpp:564: write at the last iteration and every write_frequency iterations
+        const bool write = (it + 1 == rp->end_iteration) || (write_frequency > 0 && (it + 1) % write_frequency == 0);
+        if (!write || !on_image) continue;
+        h.resize((size_t)npix * 3);
+        img.resize(h.size());
         if (hipMemcpyAsync(h.data(), ld, h.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipStreamSynchronize(c->stream) != hipSuccess)
+            hipStreamSynchronize(c->stream) != hipSuccess) {
             st = fail(c, BRE_ERR_HIP, "bre_render: copy-back failed");
-        else if (rp->end_iteration > rp->start_iteration)
-            st = bre_resolve_image(npix, h.data(), rp->end_iteration - 1, image);  // Ld / (iter + 1)
-        else
-            memset(image, 0, h.size() * sizeof(float));
+            break;
+        }
+        st = bre_resolve_image(npix, h.data(), it, img.data());  // L = Ld / (iter + 1), :578
+        if (st == BRE_OK && on_image(it, img.data(), user) != 0)
+            st = fail(c, BRE_ERR_STATE, "bre_render: image callback stopped the render after iteration %d", it);
     }
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(ld);
     return st;
+}
+
+namespace {
+struct FinalImage {
+    float *dst;
+    size_t n;
+};
+int keep_final_image(int32_t, const float *img, void *user) {
+    FinalImage *f = static_cast<FinalImage *>(user);
+    memcpy(f->dst, img, f->n * sizeof(float));
+    return 0;
+}
+}  // namespace
+
+bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_params *rp, float *image) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    bre_status st = check_params(c, rp);
+    if (st != BRE_OK) return st;
+    if (!image) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null image");
+    FinalImage f{image, (size_t)rp->width * rp->height * 3};
+    if (rp->end_iteration == rp->start_iteration) {
+        memset(image, 0, f.n * sizeof(float));
+        return BRE_OK;
+    }
+    // only the last iteration's image is kept (write_frequency 0 = at the end only)
+    return bre_render_progressive(c, scene, rp, 0, keep_final_image, &f);
 }
 
 void bre_scene_cornell(bre_scene *s, float sigma_a, float sigma_s, float g) {

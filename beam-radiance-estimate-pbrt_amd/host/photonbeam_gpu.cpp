@@ -1,6 +1,9 @@
 // photonbeam_gpu.cpp — see photonbeam_gpu.h.
 #include "photonbeam_gpu.h"
 
+#include <climits>
+#include <cstring>
+
 namespace bre_host {
 
 void SegmentRecorder::Clear() {
@@ -88,6 +91,80 @@ float BeamRadiusAt(const PhotonBeamParams &p, int iteration) {
 void ResolveImage(const std::vector<float> &pixelLd, int iteration, std::vector<float> &rgb) {
     rgb.resize(pixelLd.size());
     bre_resolve_image((int64_t)(pixelLd.size() / 3), pixelLd.data(), iteration, rgb.data());
+}
+
+PhotonBeamIntegrator::PhotonBeamIntegrator(const PhotonBeamParams &params, const FilmDesc &film, int device)
+    : params_(params), film_(film) {
+    const bre_status st = bre_create(device, &ctx_);
+    if (st != BRE_OK) {
+        ctx_ = nullptr;
+        err_ = "bre_create failed with status " + std::to_string((int)st);
+    }
+}
+
+PhotonBeamIntegrator::~PhotonBeamIntegrator() { bre_destroy(ctx_); }
+
+std::string PfmFilename(const std::string &filename) {
+    const size_t dot = filename.find_last_of('.');
+    const size_t slash = filename.find_last_of('/');
+    if (dot != std::string::npos && (slash == std::string::npos || dot > slash)) {
+        std::string ext = filename.substr(dot);
+        for (auto &c : ext) c = (char)tolower((unsigned char)c);
+        if (ext == ".pfm") return filename;
+        return filename.substr(0, dot) + ".pfm";
+    }
+    return filename + ".pfm";
+}
+
+int PhotonBeamIntegrator::OnImage(int32_t, const float *L, void *user) {
+    PhotonBeamIntegrator *self = static_cast<PhotonBeamIntegrator *>(user);
+    const int64_t npix = (int64_t)self->film_.xres * self->film_.yres;
+    self->image_.resize((size_t)npix * 3);
+    FilmFinalize(L, npix, self->film_.scale, self->image_.data());  // Film::SetImage + WriteImage
+    ++self->written_;
+    if (!self->writeFiles) return 0;
+    std::string err;
+    if (!WritePFM(PfmFilename(self->film_.filename), self->image_.data(), self->film_.xres, self->film_.yres, &err)) {
+        self->err_ = err;
+        return 1;
+    }
+    return 0;
+}
+
+bool PhotonBeamIntegrator::Render(const bre_scene &scene) {
+    if (!ctx_) return false;
+    bre_render_params rp;
+    memset(&rp, 0, sizeof(rp));
+    rp.width = film_.xres;
+    rp.height = film_.yres;
+    rp.iterations = params_.nIterations;
+    rp.start_iteration = params_.startIteration;
+    rp.end_iteration = params_.endIteration;
+    rp.photons_per_iteration = params_.photonsPerIteration;
+    rp.max_depth = params_.maxDepth;
+    rp.render_surfaces = params_.renderSurfaces;
+    rp.render_media = params_.renderMedia;
+    rp.initial_radius = params_.initialBeamRadius;
+    rp.alpha = params_.alpha;
+    written_ = 0;
+    // the reference's default 1 << 31 is INT_MIN, which never divides iter + 1: "at the end only"
+    const int32_t wf = params_.writeFrequency > 0 ? params_.writeFrequency : 0;
+    const bre_status st = bre_render_progressive(ctx_, &scene, &rp, wf, &PhotonBeamIntegrator::OnImage, this);
+    if (st != BRE_OK) {
+        if (err_.empty()) err_ = bre_last_error(ctx_);
+        return false;
+    }
+    return true;
+}
+
+std::unique_ptr<PhotonBeamIntegrator> CreatePhotonBeamIntegrator(const ParamSet &params, const FilmDesc &film,
+                                                                 bool quickRender, int device) {
+    PhotonBeamParams::Lookup lk;
+    lk.findInt = [&](const char *n, int d) { return params.FindOneInt(n, d); };
+    lk.findFloat = [&](const char *n, float d) { return params.FindOneFloat(n, d); };
+    lk.findBool = [&](const char *n, bool d) { return params.FindOneBool(n, d); };
+    const PhotonBeamParams p = PhotonBeamParams::FromLookup(lk, quickRender, film.xres * film.yres);
+    return std::unique_ptr<PhotonBeamIntegrator>(new PhotonBeamIntegrator(p, film, device));
 }
 
 }  // namespace bre_host

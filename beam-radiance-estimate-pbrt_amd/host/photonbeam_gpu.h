@@ -16,10 +16,12 @@
 
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/bre.h"
+#include "pbrt_scene.h"
 
 namespace bre_host {
 
@@ -112,5 +114,48 @@ struct PhotonBeamParams {
 float BeamRadiusAt(const PhotonBeamParams &p, int iteration);
 // L = Ld / (iter + 1) per pixel (photonbeam.cpp:578).
 void ResolveImage(const std::vector<float> &pixelLd, int iteration, std::vector<float> &rgb);
+
+// Mirror of pbrt::PhotonBeamIntegrator (photonbeam.h:18-60) with Render (photonbeam.cpp:329-586)
+// running on the GPU through bre_render_progressive: per iteration the photon pass, BVH build,
+// camera pass and gather stay in HBM; at the reference's write schedule (:564-584) the image
+// L = Ld / (iter + 1) goes through Film::SetImage + Film::WriteImage (FilmFinalize) and is
+// written to the film's file as PFM.
+class PhotonBeamIntegrator {
+  public:
+    PhotonBeamIntegrator(const PhotonBeamParams &params, const FilmDesc &film, int device = 0);
+    ~PhotonBeamIntegrator();
+    PhotonBeamIntegrator(const PhotonBeamIntegrator &) = delete;
+    PhotonBeamIntegrator &operator=(const PhotonBeamIntegrator &) = delete;
+
+    // Integrator::Render(const Scene &): false (with LastError) on any failure.
+    bool Render(const bre_scene &scene);
+    // The last image handed to the film, after WriteImage's conversion (top row first, 3 floats
+    // per pixel), and how many times the film was written.
+    const std::vector<float> &Image() const { return image_; }
+    int ImagesWritten() const { return written_; }
+    const PhotonBeamParams &Params() const { return params_; }
+    const FilmDesc &Film() const { return film_; }
+    bool writeFiles = true;  // false: keep the images in memory only (tests)
+    bre_ctx *Context() { return ctx_; }
+    const std::string &LastError() const { return err_; }
+
+  private:
+    static int OnImage(int32_t iteration, const float *L, void *self);
+    PhotonBeamParams params_;
+    FilmDesc film_;
+    bre_ctx *ctx_ = nullptr;
+    std::vector<float> image_;
+    int written_ = 0;
+    std::string err_;
+};
+
+// CreatePhotonBeamIntegrator(const ParamSet &, shared_ptr<const Camera>) (photonbeam.cpp:589-611):
+// the camera's film supplies the pixel count for photonsperiteration's default.
+std::unique_ptr<PhotonBeamIntegrator> CreatePhotonBeamIntegrator(const ParamSet &params, const FilmDesc &film,
+                                                                 bool quickRender = false, int device = 0);
+
+// The PFM name the film is written to: the film's filename with a .pfm extension (this build
+// writes PFM only; pbrt picks the writer by extension, imageio.cpp WriteImage).
+std::string PfmFilename(const std::string &filename);
 
 }  // namespace bre_host

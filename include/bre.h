@@ -202,6 +202,16 @@ bre_status bre_get_segments(bre_ctx *ctx, int64_t capacity, float *o_xyz, float 
 bre_status bre_render_iteration(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params,
                                 int32_t iteration, float *d_ld_rgb);
 bre_status bre_render(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params, float *image_rgb);
+/* The write schedule of Render (photonbeam.cpp:564-584): after iteration `iter`, when
+   iter + 1 == end_iteration or (iter + 1) % write_frequency == 0, the image L = Ld / (iter + 1)
+   (host float[3*W*H], row-major from the top row, valid only during the call) is handed to
+   `on_image(iter, L, user)`, where the reference calls Film::SetImage + Film::WriteImage.
+   write_frequency <= 0 means "only at the end" (the reference's default 1 << 31 wraps to INT_MIN,
+   which never divides iter + 1).  A non-zero return from on_image stops the render with
+   BRE_ERR_STATE.  on_image may be NULL. */
+typedef int (*bre_image_fn)(int32_t iteration, const float *image_rgb, void *user);
+bre_status bre_render_progressive(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params,
+                                  int32_t write_frequency, bre_image_fn on_image, void *user);
 
 /* ---- integrator helpers (photonbeam.cpp:354-356, 562, 578) ---- */
 /* R_i for iteration i: R_{k+1} = R_k * (k + alpha) / (k + 1), R_0 = initial, in float. */
