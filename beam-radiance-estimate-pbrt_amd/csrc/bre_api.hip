@@ -61,6 +61,7 @@ struct bre_ctx {
     int debug_mode = 0;
     int stack_limit = 0;
     int occupancy = 0;
+    int tile_mode = 1;       // kernel 4: prefilter-first leaf scan (1) or box-first (0)
     float loose_cos = 0.f;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
@@ -367,6 +368,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.debug_mode = c->debug_mode;
     a.stack_limit = c->stack_limit;
     a.occupancy = c->occupancy;
+    a.tile_mode = c->tile_mode;
     a.loose_cos = c->loose_cos;
     a.roots = nullptr;
     a.partial = nullptr;
@@ -559,6 +561,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
     case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
     case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 3 register budget
+    case 104: c->tile_mode = (int)value; return BRE_OK;    // internal: kernel 4 leaf order (tests, sweeps)
     case 103: c->loose_cos = (float)value * 1e-4f; return BRE_OK;  // internal: kernel 3 coherence cut (1e-4)
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }

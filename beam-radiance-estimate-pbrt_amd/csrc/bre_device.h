@@ -127,6 +127,7 @@ struct GatherArgs {
     int leaf2;
     float loose_cos;       // kernel 3: packets whose lanes' directions spread wider than this cosine
                            // are handed over (0: default)
+    int tile_mode;         // kernel 4 leaf order: 0 box test first, 1 line-distance prefilter first
 };
 
 // capsule-chunk index (bre_chunk.hip)

@@ -485,8 +485,9 @@ __device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, in
     float te;
     bool hit = on & node_test(box, o, invs, tmax, te);
     if (__ballot(on & inf) != 0ull) {
+        // shuffle with every lane active: ds_bpermute reads 0 from a lane outside EXEC
+        const f3 d = mk(__shfl(M.d.x, sl), __shfl(M.d.y, sl), __shfl(M.d.z, sl));
         if (on & inf) {
-            const f3 d = mk(__shfl(M.d.x, sl), __shfl(M.d.y, sl), __shfl(M.d.z, sl));
             const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
             hit = slab_test(box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
         }
@@ -819,6 +820,54 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, const Lane &M, int fi
     }
 }
 
+// Prefilter-first stage 2: the reference's box test on the beam's (group) box, then exact closest
+// points + kernel, for n queued prefilter survivors (one per lane; all lanes call).  The pair's
+// beam line comes from L2 (the staged tile may already be replaced).
+template <bool COUNT>
+__device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, int first, int n,
+                                               const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                               float R, Prof &pf) {
+    const int lane = threadIdx.x & 63;
+    const bool on = lane < n;
+    const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
+    const int32_t b = sh.qb1[e];
+    const int sl = sh.ql1[e];
+    const f3 o = mk(lane_f(M.o.x, sl), lane_f(M.o.y, sl), lane_f(M.o.z, sl));
+    const f3 invs = mk(lane_f(M.invs.x, sl), lane_f(M.invs.y, sl), lane_f(M.invs.z, sl));
+    const float tmax = lane_f(M.tmax, sl);
+    const BeamV r = load_beam(recs, b);
+    if (COUNT && lane == 0) ++pf.ccp_waves;
+    float te;
+    bool hit = on & node_test(r.box, o, invs, tmax, te);
+    const bool inf = __shfl((int)M.has_inf, sl) != 0;
+    if (__ballot(on & inf) != 0ull) {
+        // shuffle with every lane active: ds_bpermute reads 0 from a lane outside EXEC
+        const f3 d = mk(lane_f(M.d.x, sl), lane_f(M.d.y, sl), lane_f(M.d.z, sl));
+        if (on & inf) {
+            const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+            hit = slab_test(r.box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
+        }
+    }
+    if (__ballot(hit) == 0ull) return;
+    const f3 p = mk(lane_f(M.p.x, sl), lane_f(M.p.y, sl), lane_f(M.p.z, sl));
+    const f3 au = mk(lane_f(M.au.x, sl), lane_f(M.au.y, sl), lane_f(M.au.z, sl));
+    const float mag_a = lane_f(M.mag_a, sl);
+    if (hit) {
+        const float maxd = R + r.radius;  // MaxDistance = currentBeamRadius + beam->radius
+        float dist;
+        const bool ok = closest_distance(o, p, au, mag_a, r.b0, r.bu, r.mag_b, dist);
+        if (ok & (dist < maxd)) {
+            const float rr = dist / maxd;
+            const float w = sqrtf(1.0f - rr * rr);
+            const float4 pv = pw[b];
+            atomicAdd(&sh.acc[0][sl], pv.x * w);
+            atomicAdd(&sh.acc[1][sl], pv.y * w);
+            atomicAdd(&sh.acc[2][sl], pv.z * w);
+            if (COUNT) atomicAdd(&sh.cnt[sl], 1);
+        }
+    }
+}
+
 // Stage 2: prefilter n box-hit pairs of the staged tile (one per lane; all lanes call); the
 // survivors are appended to queue 1, which is drained in batches of 64.  Without the prefilter,
 // every pair is forwarded.
@@ -863,7 +912,7 @@ __device__ __forceinline__ void tile_filter(TileShared &sh, const Lane &M, int f
     }
 }
 
-template <bool COUNT, bool PREF, int MINW>
+template <bool COUNT, bool PREF, int MINW, bool PFIRST>
 __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
@@ -930,6 +979,48 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            if (PFIRST) {
+                // prefilter first: per lane and beam only the conservative line-distance bound
+                // (lanes that miss the tile's node box miss every beam box in it); survivors go
+                // to queue 1 with their global beam index and run box test + exact 64 at a time.
+                // Queue order is (leaf, beam, lane) as in the box-first order, so each segment
+                // sums the same pairs in the same order (bit-identical to tile_mode 0).
+                for (int j = 0; j < nb; ++j) {
+                    const float4 y = sh.tile[j][1], z = sh.tile[j][2], wv = sh.tile[j][3];
+                    bool need = lane_on;
+                    if (PREF)
+                        need = lane_on && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, mk(y.z, y.w, z.x),
+                                                               mk(z.y, z.z, z.w), R + wv.y);
+                    if (COUNT) {
+                        const float4 x = sh.tile[j][0];
+                        const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+                        float te;
+                        bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
+                        if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
+                        cand += hit;
+                        pf.rejects += hit & !need;
+                    }
+                    const unsigned long long m = __ballot(need);
+                    if (m == 0ull) continue;
+                    if (need) {
+                        const int pos = (t1 + lanes_below(m)) & (kQueueCap - 1);
+                        sh.qb1[pos] = (int32_t)(tile0 + j);
+                        sh.ql1[pos] = (uint8_t)lane;
+                    }
+                    t1 += __popcll(m);
+                    __builtin_amdgcn_wave_barrier();
+                    if (t1 - h1 >= 64) {
+                        if (dbg != 2) tile_box_exact<COUNT>(sh, L, h1, 64, recs, pw, R, pf);
+                        h1 += 64;
+                        if (h1 >= 1024) {
+                            h1 -= 1024;
+                            t1 -= 1024;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                continue;
+            }
             for (int j = 0; j < nb; ++j) {
                 const float4 x = sh.tile[j][0], y = sh.tile[j][1];
                 const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
@@ -1014,7 +1105,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         }
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
-        if (dbg != 2 && t1 > h1) tile_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
+        if (dbg != 2 && t1 > h1) {
+            if (PFIRST) tile_box_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
+            else tile_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
+        }
         h1 = t1 = 0;
     }
     __builtin_amdgcn_wave_barrier();
@@ -1267,16 +1361,18 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         const int leaf4 = ho ? a.leaf2 : a.leaf_size;
         const uint8_t *redo4 = ho ? a.redo : nullptr;
         const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
-#define BRE_LAUNCH_TILE_W(C, P, W)                                                                                \
-    hipLaunchKernelGGL((k_gather_tile<C, P, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R, \
+#define BRE_LAUNCH_TILE_W(C, P, W, F)                                                                             \
+    hipLaunchKernelGGL((k_gather_tile<C, P, W, F>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R, \
                        a.partial, a.pcnt, a.recs, a.pow, nodes4, a.nvalid, leaf4, roots4, a.split,                   \
                        a.ctr, a.debug_mode, redo4)
 #define BRE_LAUNCH_TILE(C, P)                      \
     do {                                           \
-        if (a.occupancy >= 8)                      \
-            BRE_LAUNCH_TILE_W(C, P, 8);            \
+        if (a.tile_mode == 1)                      \
+            BRE_LAUNCH_TILE_W(C, P, 1, true);      \
+        else if (a.occupancy >= 8)                 \
+            BRE_LAUNCH_TILE_W(C, P, 8, false);     \
         else                                       \
-            BRE_LAUNCH_TILE_W(C, P, 1);            \
+            BRE_LAUNCH_TILE_W(C, P, 1, false);     \
     } while (0)
         if (counters) {
             if (a.prefilter) BRE_LAUNCH_TILE(true, true);

@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--loose-cos", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--tile-mode", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -141,6 +142,8 @@ def main():
         g.set_option(103, args.loose_cos)
     if args.tile_leaf:
         g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
+    if args.tile_mode >= 0:
+        g.set_option(104, args.tile_mode)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)

@@ -330,3 +330,26 @@ def test_auto_handover_mixed_packets(bre, synth, oracle, tile_leaf):
     assert np.array_equal(out["counts"][:, 1], ref["contrib"])
     assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
     assert _rel_l2(accum, ref["accum"]) <= 1e-6
+
+
+@pytest.mark.parametrize("leaf", [16, 32])
+def test_kernel4_leaf_orders_are_bit_identical(bre, synth, oracle, leaf):
+    """Kernel 4's prefilter-first leaf scan (tile_mode 1, default) and box-first scan (0) queue the
+    contributing pairs in the same (leaf, beam, lane) order: same counts, bit-identical sums, and
+    both exact against the oracle (including axis-parallel rays, which take the slab test)."""
+    beams = synth.fog_beams(6000, seed=81, radius=0.03, mean_length=0.6)
+    segs = synth.bounce_segments(2500, seed=82)
+    segs["d"][::97] = np.array([0.0, 0.0, 1.0], np.float32)  # axis-parallel rays (infinite 1/d)
+    segs["p"][::97] = segs["o"][::97] + segs["tmax"][::97, None] * segs["d"][::97]
+    ref = oracle.build(beams).gather(segs, 0.04)
+    outs = []
+    for mode in (0, 1):
+        with bre.BeamGather(0, counters=True, kernel=4, leaf_size=leaf) as g:
+            g.set_option(104, mode)
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.04, counts=True))
+    for o in outs:
+        assert np.array_equal(o["counts"][:, 0], ref["cand"])
+        assert np.array_equal(o["counts"][:, 1], ref["contrib"])
+        assert _seg_close(o["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    assert np.array_equal(outs[0]["seg_rgb"], outs[1]["seg_rgb"])
