@@ -60,7 +60,8 @@ struct bre_ctx {
     bool prefilter = true;
     int debug_mode = 0;
     int stack_limit = 0;
-    int occupancy = 0;
+    int occupancy = 8;       // kernel 4 register budget (min waves per SIMD): 8 measured best at C2
+    int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int tile_mode = 1;       // kernel 4: prefilter-first leaf scan (1) or box-first (0)
     float loose_cos = 0.f;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
@@ -560,8 +561,9 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         return BRE_OK;
     case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
     case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
-    case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 3 register budget
+    case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 4 register budget (1 or 8)
     case 104: c->tile_mode = (int)value; return BRE_OK;    // internal: kernel 4 leaf order (tests, sweeps)
+    case 105: c->sort_key = (int)value; return BRE_OK;     // internal: segment sort key (sweeps)
     case 103: c->loose_cos = (float)value * 1e-4f; return BRE_OK;  // internal: kernel 3 coherence cut (1e-4)
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
@@ -879,7 +881,7 @@ bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
                c->seg_pix.as<int32_t>(), c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
                c->ss_keys_alt.as<unsigned long long>(), c->ss_vals.as<int32_t>(), c->ss_vals_alt.as<int32_t>(),
                c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
-               c->ss_t.as<float>(), c->ss_pix.as<int32_t>()};
+               c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
     return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, nullptr, nullptr);
 }

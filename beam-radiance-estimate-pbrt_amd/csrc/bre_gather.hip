@@ -1367,7 +1367,9 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
                        a.ctr, a.debug_mode, redo4)
 #define BRE_LAUNCH_TILE(C, P)                      \
     do {                                           \
-        if (a.tile_mode == 1)                      \
+        if (a.tile_mode == 1 && a.occupancy >= 8)  \
+            BRE_LAUNCH_TILE_W(C, P, 8, true);      \
+        else if (a.tile_mode == 1)                 \
             BRE_LAUNCH_TILE_W(C, P, 1, true);      \
         else if (a.occupancy >= 8)                 \
             BRE_LAUNCH_TILE_W(C, P, 8, false);     \

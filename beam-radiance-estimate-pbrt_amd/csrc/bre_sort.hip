@@ -7,7 +7,9 @@
 // directions: a packet of 64 unrelated rays visits the union of 64 traversals.  Sorting by a 5-D
 // Morton key of (origin in the segments' box, octahedral direction) puts segments that start
 // close together AND point the same way into the same packet, so the packet kernels share most
-// of their node and beam visits again.  Only the order changes; every per-segment sum and every
+// of their node and beam visits again.  The default key (mode 1) interleaves the segment's origin
+// and end point instead (6-D Morton): two segments with both ends close are close all along, which
+// at C2 shortens the gather by ~5% over the (origin, direction) key (mode 0).  Only the order changes; every per-segment sum and every
 // pixel total is the same set of pair contributions.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -37,6 +39,7 @@ __global__ void k_sort_init(unsigned int *b) {
 
 __global__ __launch_bounds__(kBlock) void k_origin_bounds(int64_t n, const float *__restrict__ o,
                                                           unsigned int *__restrict__ b) {
+    // (key mode 1 launches it twice, over the origins and the end points, into one box)
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
     bool any = false;
@@ -112,6 +115,31 @@ __global__ __launch_bounds__(kBlock) void k_seg_keys(int64_t n, const float *__r
     vals[i] = (int32_t)i;
 }
 
+// 6-D Morton key: 10 bits each of origin x, y, z and end point x, y, z (in the box of both)
+__global__ __launch_bounds__(kBlock) void k_seg_keys_op(int64_t n, const float *__restrict__ o,
+                                                        const float *__restrict__ p, const unsigned int *__restrict__ b,
+                                                        unsigned long long *__restrict__ keys,
+                                                        int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float lo[3] = {ord2f(b[0]), ord2f(b[1]), ord2f(b[2])};
+    const float hi[3] = {ord2f(b[3]), ord2f(b[4]), ord2f(b[5])};
+    unsigned int q[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float ext = hi[k] - lo[k];
+        q[k] = quant10(ext > 0.f ? (o[3 * i + k] - lo[k]) / ext : 0.f);
+        q[3 + k] = quant10(ext > 0.f ? (p[3 * i + k] - lo[k]) / ext : 0.f);
+    }
+    unsigned long long key = 0ull;
+#pragma unroll
+    for (int bit = 9; bit >= 0; --bit)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
 __global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t *__restrict__ order,
                                                         const float *__restrict__ o, const float *__restrict__ p,
                                                         const float *__restrict__ d, const float *__restrict__ t,
@@ -138,7 +166,7 @@ inline unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 size_t seg_sort_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 50);
+                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 60);
     return bytes;
 }
 
@@ -146,11 +174,18 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     if (s.n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sort_init, dim3(1), dim3(64), 0, st, s.bounds);
     hipLaunchKernelGGL(k_origin_bounds, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
-    hipLaunchKernelGGL(k_seg_keys, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.d, s.bounds, s.keys, s.vals);
+    if (s.key_mode == 1) {
+        hipLaunchKernelGGL(k_origin_bounds, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
+        hipLaunchKernelGGL(k_seg_keys_op, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.bounds, s.keys,
+                           s.vals);
+    } else {
+        hipLaunchKernelGGL(k_seg_keys, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.d, s.bounds, s.keys,
+                           s.vals);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.tmp_bytes;
-    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, 50, st);
+    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, s.key_mode == 1 ? 60 : 50, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
                        s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);

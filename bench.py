@@ -75,6 +75,7 @@ def parse():
     ap.add_argument("--loose-cos", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-mode", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -144,6 +145,8 @@ def main():
         g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
     if args.tile_mode >= 0:
         g.set_option(104, args.tile_mode)
+    if args.sort_key >= 0:
+        g.set_option(105, args.sort_key)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
