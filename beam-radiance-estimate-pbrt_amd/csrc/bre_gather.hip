@@ -374,6 +374,67 @@ __device__ __forceinline__ Proxy make_proxy(const Lane &L, bool valid) {
     return P;
 }
 
+// Packet bundle for kernel 3's packet-level line-distance reject.  A line C (point co, unit
+// direction cu) and delta >= the distance of every valid lane's segment END POINTS from C.  The
+// distance to a line is convex along a segment, so every point of every lane's segment lies within
+// delta of C, and for any beam line B: dist(segment_i, B) >= dist(C, B) - delta.  One lane-wide
+// evaluation per beam (64 beams at once) then rejects a beam for all 64 segments, before the
+// per-lane prefilter.  delta and the coordinate bound are inflated for rounding.
+struct Bundle {
+    f3 co, cu;
+    float delta;  // FLT_MAX disables the test
+    float omax;   // max over valid lanes of Lane::omax (bounds every segment-side coordinate)
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
+    Bundle K;
+    const float n = (float)__popcll(__ballot(valid));
+    K.co = mk(wave_sum(valid ? L.o.x : 0.f) / n, wave_sum(valid ? L.o.y : 0.f) / n, wave_sum(valid ? L.o.z : 0.f) / n);
+    const f3 su = mk(wave_sum(valid ? L.au.x : 0.f), wave_sum(valid ? L.au.y : 0.f), wave_sum(valid ? L.au.z : 0.f));
+    const float sl = sqrtf(lensq3(su));
+    K.omax = wave_max(valid ? L.omax : 0.f);
+    if (!(sl > 0.f) || !isfinite(sl)) {
+        K.cu = mk(0.f, 0.f, 1.f);
+        K.delta = FLT_MAX;
+        return K;
+    }
+    K.cu = mk(su.x / sl, su.y / sl, su.z / sl);
+    const auto perp = [&](f3 x) {
+        const f3 t = sub3(x, K.co);
+        const f3 c = mk(t.y * K.cu.z - t.z * K.cu.y, t.z * K.cu.x - t.x * K.cu.z, t.x * K.cu.y - t.y * K.cu.x);
+        return sqrtf(lensq3(c));
+    };
+    const float dl = valid ? fmaxf(perp(L.o), perp(L.p)) : 0.f;
+    const float cm = fmaxf(fmaxf(fabsf(K.co.x), fabsf(K.co.y)), fabsf(K.co.z));
+    const float d = wave_max(dl);
+    K.delta = isfinite(d) ? d * 1.0001f + 1e-5f * (K.omax + cm) + 1e-6f : FLT_MAX;
+    return K;
+}
+
+// far_from_lines_fast's bound for the bundle's line against a beam line, with maxd + delta: a
+// rejection proves that every lane's computed ComputeClosestPoints distance is >= maxd.
+__device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float maxd) {
+    if (!(K.delta < 1e30f)) return false;
+    const f3 t = sub3(b0, K.co);
+    const f3 n = mk(__builtin_fmaf(K.cu.y, bu.z, -(K.cu.z * bu.y)), __builtin_fmaf(K.cu.z, bu.x, -(K.cu.x * bu.z)),
+                    __builtin_fmaf(K.cu.x, bu.y, -(K.cu.y * bu.x)));
+    const float nn = __builtin_fmaf(n.x, n.x, __builtin_fmaf(n.y, n.y, n.z * n.z));
+    if (!(nn >= 1e-2f)) return false;
+    const float tn = fabsf(__builtin_fmaf(t.x, n.x, __builtin_fmaf(t.y, n.y, t.z * n.z)));
+    const float tl = fabsf(t.x) + fabsf(t.y) + fabsf(t.z);
+    const float bmax = fmaxf(fmaxf(fabsf(b0.x), fabsf(b0.y)), fabsf(b0.z));
+    const float mag = K.omax + bmax + 10.0f * tl + maxd + 1.0f;
+    const float eps = 1e-5f * mag + 1e-6f;
+    const float nl = __builtin_amdgcn_sqrtf(nn) * 1.000001f;
+    return (tn - 1e-6f * tl) > ((maxd + K.delta) * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
+}
+
 __device__ __forceinline__ float min4(float a, float b, float c, float d) { return fminf(fminf(a, b), fminf(c, d)); }
 __device__ __forceinline__ float max4(float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); }
 
@@ -457,8 +518,8 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
 constexpr int kPQueue = 128;  // >= 63 left over + 64 appended by one beam
 
 struct ProxyQ {
-    float4 bst[64][4];     // staged BeamRec lines of the current batch
-    float4 bpw[64];        // their scaled powers
+    float4 bst[64][2];     // staged lines of the current batch: (b0, |B|), (unit dir, radius)
+    int32_t gid[64];       // their beam indices (box and power are read from L2 by pq_exact)
     float acc[3][64];      // per-segment RGB
     int32_t cnt[64];       // per-segment contribution counts (counters only)
     uint16_t q[kPQueue];   // ring: staged slot | segment lane << 8
@@ -466,7 +527,8 @@ struct ProxyQ {
 
 // all lanes call; lanes < n take pair (first + lane) of the ring
 template <bool COUNT>
-__device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, int n, float R, Prof &pf) {
+__device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, int n, float R,
+                                         const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, Prof &pf) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
     const unsigned qv = q.q[(first + (on ? lane : 0)) & (kPQueue - 1)];
@@ -478,8 +540,9 @@ __device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, in
     const float mag_a = __shfl(M.mag_a, sl);
     const float tmax = __shfl(M.tmax, sl);
     const bool inf = __shfl((int)M.has_inf, sl) != 0;
-    const float4 x = q.bst[j][0], y = q.bst[j][1], z = q.bst[j][2], w = q.bst[j][3];
-    const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+    const int32_t bi = q.gid[j];
+    const BeamV r = load_beam(recs, bi);  // one 64-B line per lane, L2-resident
+    const Box6 &box = r.box;
     if (COUNT && lane == 0) ++pf.ccp_waves;
     // the reference's candidate test on the beam's (group) box, as eval_beam
     float te;
@@ -494,14 +557,13 @@ __device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, in
     }
     if (__ballot(hit) == 0ull) return;
     if (hit) {
-        const f3 b0 = mk(y.z, y.w, z.x), bu = mk(z.y, z.z, z.w);
-        const float maxd = R + w.y;  // MaxDistance = currentBeamRadius + beam->radius
+        const float maxd = R + r.radius;  // MaxDistance = currentBeamRadius + beam->radius
         float dist;
-        const bool ok = closest_distance(o, p, au, mag_a, b0, bu, w.x, dist);
+        const bool ok = closest_distance(o, p, au, mag_a, r.b0, r.bu, r.mag_b, dist);
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
             const float wt = sqrtf(1.0f - rr * rr);
-            const float4 pv = q.bpw[j];
+            const float4 pv = pw[bi];
             atomicAdd(&q.acc[0][sl], pv.x * wt);
             atomicAdd(&q.acc[1][sl], pv.y * wt);
             atomicAdd(&q.acc[2][sl], pv.z * wt);
@@ -513,30 +575,54 @@ __device__ __forceinline__ void pq_exact(ProxyQ &q, const Lane &M, int first, in
 template <bool COUNT, bool PREF>
 __device__ __forceinline__ void proxy_batch_q(ProxyQ &q, const Lane &L, bool valid, const int32_t *cand, int nb,
                                               const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
-                                              float R, int &ccount, Prof &pf, int dbg) {
+                                              float R, int &ccount, Prof &pf, int dbg, const Bundle &K) {
     const int lane = threadIdx.x & 63;
+    // stage the batch, lane j holding beam j; the packet-level bundle test (one beam per lane)
+    // drops beams that are far from every segment of the packet.  Kept beams are compacted in
+    // candidate order (COUNT: all are staged, dropped ones flagged by ~index, because the
+    // reference's candidate count needs every box test).
+    int32_t bi = 0;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    bool keep = false;
     if (lane < nb) {
-        const int32_t bi = cand[lane];
+        bi = cand[lane];
         const float4 *src = reinterpret_cast<const float4 *>(recs + bi);
-        const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = pw[bi];
-        q.bst[lane][0] = a;
-        q.bst[lane][1] = b;
-        q.bst[lane][2] = c;
-        q.bst[lane][3] = d;
-        q.bpw[lane] = e;
+        const float4 b = src[1], c = src[2], d = src[3];
+        s0 = make_float4(b.z, b.w, c.x, d.x);  // b0, |B|
+        s1 = make_float4(c.y, c.z, c.w, d.y);  // unit dir, radius
+        keep = !(PREF && bundle_far(K, mk(s0.x, s0.y, s0.z), mk(s1.x, s1.y, s1.z), R + s1.w));
+    }
+    int nk;
+    if (COUNT) {
+        if (lane < nb) {
+            q.bst[lane][0] = s0;
+            q.bst[lane][1] = s1;
+            q.gid[lane] = keep ? bi : ~bi;
+        }
+        nk = nb;
+    } else {
+        const unsigned long long km = __ballot(keep);
+        if (keep) {
+            const int pos = lanes_below(km);
+            q.bst[pos][0] = s0;
+            q.bst[pos][1] = s1;
+            q.gid[pos] = bi;
+        }
+        nk = __popcll(km);
     }
     if (COUNT) pf.beams += nb;
     __builtin_amdgcn_wave_barrier();
     int qh = 0, qt = 0;  // wave-uniform ring head / tail (the ring is drained per batch)
-    for (int j = 0; j < nb; ++j) {
-        const float4 y = q.bst[j][1], z = q.bst[j][2], w = q.bst[j][3];
-        const f3 b0 = mk(y.z, y.w, z.x), bu = mk(z.y, z.z, z.w);
+    for (int j = 0; j < nk; ++j) {
+        const float4 y = q.bst[j][0], z = q.bst[j][1];
+        const f3 b0 = mk(y.x, y.y, y.z), bu = mk(z.x, z.y, z.z);
         bool need = valid;
-        if (PREF) need = valid && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, b0, bu, R + w.y);
+        if (COUNT) need = need && q.gid[j] >= 0;
+        if (PREF) need = need && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, b0, bu, R + z.w);
         if (COUNT) {
             // the reference's candidate count C (box hits), for the parity tests
-            const float4 x = q.bst[j][0];
-            const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+            const int32_t g = q.gid[j];
+            const Box6 box = load_beam(recs, g >= 0 ? g : ~g).box;
             float te;
             bool hit = valid & node_test(box, L.o, L.invs, L.tmax, te);
             if (L.has_inf) hit = valid & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
@@ -549,12 +635,12 @@ __device__ __forceinline__ void proxy_batch_q(ProxyQ &q, const Lane &L, bool val
         qt += __popcll(m);
         __builtin_amdgcn_wave_barrier();
         if (qt - qh >= 64) {
-            if (dbg != 2) pq_exact<COUNT>(q, L, qh, 64, R, pf);
+            if (dbg != 2) pq_exact<COUNT>(q, L, qh, 64, R, recs, pw, pf);
             qh += 64;
             __builtin_amdgcn_wave_barrier();
         }
     }
-    if (qt > qh && dbg != 2) pq_exact<COUNT>(q, L, qh, qt - qh, R, pf);
+    if (qt > qh && dbg != 2) pq_exact<COUNT>(q, L, qh, qt - qh, R, recs, pw, pf);
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -615,6 +701,7 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
         // handed to kernel 1 (depth-first per-lane traversal), which runs behind this launch
     } else if (__ballot(valid) != 0ull) {
         const Proxy P = make_proxy(L, valid);
+        const Bundle K = make_bundle(L, valid);
         const int32_t root = roots[sub];
         int sp = 0, nc = 0;
         if (root < 0) {
@@ -649,7 +736,7 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
             while (nc >= 64) {
                 nc -= 64;
                 if (dbg != 1)  // dbg 1: timing-only traversal
-                    proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, 64, recs, pw, R, ccount, pf, dbg);
+                    proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, 64, recs, pw, R, ccount, pf, dbg, K);
                 __builtin_amdgcn_wave_barrier();
             }
             // 3. test the popped nodes' children against the packet proxy
@@ -698,7 +785,7 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
                     const int nb = min(64, nc);
                     nc -= nb;
                     if (dbg != 1)
-                        proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, nb, recs, pw, R, ccount, pf, dbg);
+                        proxy_batch_q<COUNT, PREF>(pq, L, valid, cand + nc, nb, recs, pw, R, ccount, pf, dbg, K);
                     __builtin_amdgcn_wave_barrier();
                 }
             }
