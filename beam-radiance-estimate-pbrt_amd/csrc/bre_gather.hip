@@ -1030,6 +1030,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     }
     Lane L;
     const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
+    Bundle K;
+    K.delta = FLT_MAX;
+    if (PFIRST && PREF && __ballot(valid) != 0ull) K = make_bundle(L, valid);
     sh.acc[0][lane] = 0.f;
     sh.acc[1][lane] = 0.f;
     sh.acc[2][lane] = 0.f;
@@ -1072,12 +1075,27 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 // to queue 1 with their global beam index and run box test + exact 64 at a time.
                 // Queue order is (leaf, beam, lane) as in the box-first order, so each segment
                 // sums the same pairs in the same order (bit-identical to tile_mode 0).
-                for (int j = 0; j < nb; ++j) {
+                // packet-level bundle reject, one beam per lane (see make_bundle): beams far from
+                // every segment of the packet are skipped by all lanes
+                unsigned long long km = ~0ull;
+                if (PREF) {
+                    bool keep = false;
+                    if (lane < nb) {
+                        const float4 y = sh.tile[lane][1], z = sh.tile[lane][2], wv = sh.tile[lane][3];
+                        keep = !bundle_far(K, mk(y.z, y.w, z.x), mk(z.y, z.z, z.w), R + wv.y);
+                    }
+                    km = __ballot(keep);
+                }
+                unsigned long long todo = COUNT ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull))
+                                                : (km & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)));
+                while (todo != 0ull) {
+                    const int j = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1ull;
                     const float4 y = sh.tile[j][1], z = sh.tile[j][2], wv = sh.tile[j][3];
-                    bool need = lane_on;
+                    bool need = lane_on && ((km >> j) & 1ull);
                     if (PREF)
-                        need = lane_on && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, mk(y.z, y.w, z.x),
-                                                               mk(z.y, z.z, z.w), R + wv.y);
+                        need = need && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, mk(y.z, y.w, z.x),
+                                                            mk(z.y, z.z, z.w), R + wv.y);
                     if (COUNT) {
                         const float4 x = sh.tile[j][0];
                         const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
