@@ -66,7 +66,7 @@ struct bre_ctx {
     float loose_cos = 0.f;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
-    int leaf2 = 32;          // auto mode: leaf size of the tile tree kernel 4 takes hand-overs on
+    int leaf2 = 64;          // auto mode: leaf size of the tile tree kernel 4 takes hand-overs on (64 best at C2)
     int built_leaf2 = 0;     // 0: no tile tree for the current beam set
     int roots2_split = -1;
     DevMem nodes2, roots2;

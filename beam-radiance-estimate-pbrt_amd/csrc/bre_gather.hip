@@ -860,7 +860,7 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
 // contributions differs (deterministic: queue order is fixed by the traversal).
 constexpr int kTileBlock = 256;  // 4 waves
 constexpr int kQueueCap = 128;   // >= 63 left over + 64 appended by one beam / one flush
-constexpr int kTileMax = 32;     // beams staged in LDS at a time (longer leaves go in chunks)
+constexpr int kTileMax = 32;     // beams staged in LDS at a time (longer leaves go in chunks; 64 costs occupancy)
 
 struct TileShared {
     float4 tile[kTileMax][4];  // staged BeamRec lines of the current leaf chunk
@@ -1059,9 +1059,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int64_t tile0 = first + base;
             __builtin_amdgcn_wave_barrier();
             {
-                // 64 lanes copy nb lines of 4 x 16 B: lane -> (beam lane >> 1, half lane & 1)
-                const int bj = lane >> 1, h = (lane & 1) * 2;
-                if (bj < nb) {
+                // 64 lanes copy nb lines of 4 x 16 B: item r -> (beam r >> 1, half r & 1)
+                for (int r = lane; r < 2 * nb; r += 64) {
+                    const int bj = r >> 1, h = (r & 1) * 2;
                     const float4 *q = reinterpret_cast<const float4 *>(recs + tile0 + bj);
                     const float4 u = q[h], v = q[h + 1];
                     sh.tile[bj][h] = u;
