@@ -103,7 +103,16 @@ WORKLOADS = {
 }
 
 
-KERNEL_NAMES = {0: "auto (packet-proxy + depth-first hand-over)", 1: "depth-first wave-packet",
+# V (reference-tree node tests) and C (candidates) per estimate of each workload's iteration 0,
+# measured by the oracle at N=1 (bench.py's CPU leg, profiles/r06/bench.json); used for the
+# roofline fields when this run has no CPU leg.  The beams and segments do not depend on N.
+ROOFLINE_REF = {
+    "c2": {"V_ref_tree": 1367176.4778887304, "C": 421298.4957203994,
+           "source": "profiles/r06/bench.json (oracle SAH tree, CPU sample of iteration 0)"},
+}
+
+
+KERNEL_NAMES = {0: "auto (packet-proxy kernel 3 + leaf-tile kernel 4 hand-over)", 1: "depth-first wave-packet",
                 2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over",
                 4: "leaf tiles + wavefront-compacted pair queue",
                 5: "capsule-chunk index (contributing pairs only)"}
@@ -232,16 +241,13 @@ def main():
     }
     result.update(diag)
 
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(wl.cpu_beams(), wl.cpu_segments(), wl.cpu_radius(), args.cpu_seconds, wl.name)
-        result["cpu_baseline"] = cpu["report"]
+    def roofline(v_ref, c_ref, source):
         # SURVEY.md §8d algorithmic bytes per estimate: 32 + 12 + 32*V + 40*C, V and C from the
-        # reference SAH tree (oracle) on the CPU sample
-        v_ref, c_ref = cpu["visit_mean"], cpu["cand_mean"]
+        # reference SAH tree (oracle) on a CPU sample of the same workload
         bytes_per_est = 32 + 12 + 32 * v_ref + 40 * c_ref
         per_launch = bytes_per_est * wl.segments_per_gather()
         achieved = per_launch / (gather_ms * 1e-3) / 1e9
-        result["roofline"] = {
+        return {
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
@@ -252,9 +258,21 @@ def main():
             "bytes_per_estimate": bytes_per_est,
             "V_ref_tree": v_ref,
             "C": c_ref,
+            "V_C_source": source,
             "kernel": "gather (k_gather_proxy + k_gather_tile hand-over)",
         }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(wl.cpu_beams(), wl.cpu_segments(), wl.cpu_radius(), args.cpu_seconds, wl.name)
+        result["cpu_baseline"] = cpu["report"]
+        result["roofline"] = roofline(cpu["visit_mean"], cpu["cand_mean"], "oracle SAH tree on this run's CPU sample")
         result["speedup_vs_cpu"] = value / cpu["report"]["value"]
+    elif rank == 0:
+        # no CPU leg (N > 1, or --no-cpu): V and C of the same workload from the committed N=1 run
+        ref = ROOFLINE_REF.get(args.workload) if (args.photons, args.width) == (
+            WORKLOADS[args.workload]["photons"], WORKLOADS[args.workload]["width"]) else None
+        if ref:
+            result["roofline"] = roofline(ref["V_ref_tree"], ref["C"], ref["source"])
     g.close()
     if rank == 0:
         line = json.dumps(result)
@@ -358,7 +376,7 @@ class SceneWorkload:
     def default_profile(self):
         if self.name != "c2":
             return None
-        return os.path.join(ROOT, "profiles", "r05", "profile_summary.json")
+        return os.path.join(ROOT, "profiles", "r06", "profile_summary.json")
 
     def config(self):
         a = self.args

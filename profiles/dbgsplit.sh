@@ -16,7 +16,8 @@ out = []
 for r in rows:
     n = r["Name"]
     if "gather" in n or "k_reduce" in n or "k_chunk" in n:
-        out.append(f'{n.split("(")[0].replace("void bre::(anonymous namespace)::", "")}: {float(r["AverageNs"])/1e6:.1f} ms x{r["Calls"]}')
+        short = n.replace("void ", "").replace("bre::(anonymous namespace)::", "").split("(")[0]
+        out.append(f'{short}: {float(r["AverageNs"])/1e6:.1f} ms x{r["Calls"]}')
 print("mode", sys.argv[2], "|", "; ".join(out))
 PY
 done

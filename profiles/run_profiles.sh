@@ -10,12 +10,12 @@ shift || true
 ARGS=("$@")
 if [ ${#ARGS[@]} -eq 0 ]; then ARGS=(--steps 5 --warmup 1); fi
 mkdir -p "$OUT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py "${ARGS[@]}" --no-cpu > "$OUT/bench_trace.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 bench.py "${ARGS[@]}" --no-cpu > "$OUT/bench_fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
-    python3 bench.py "${ARGS[@]}" --no-cpu > "$OUT/bench_write.log" 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py "${ARGS[@]}" --no-cpu --no-diag > "$OUT/bench_trace.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- \
+    python3 bench.py "${ARGS[@]}" --no-cpu --no-diag > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
+    python3 bench.py "${ARGS[@]}" --no-cpu --no-diag > "$OUT/bench_write.log" 2>&1
 python3 profiles/summarize.py "$OUT" "$OUT/profile_summary.json" > "$OUT/summary.log"
 cp "$OUT/trace/run_kernel_stats.csv" "$OUT/kernel_stats.csv"
 echo "profiles done"
