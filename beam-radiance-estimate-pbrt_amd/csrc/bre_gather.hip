@@ -386,25 +386,36 @@ struct Bundle {
     float omax;   // max over valid lanes of Lane::omax (bounds every segment-side coordinate)
 };
 
-__device__ __forceinline__ float wave_sum(float v) {
+template <int G>
+__device__ __forceinline__ float grp_sum(float v) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ float grp_max(float v) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
     return v;
 }
 
-__device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
+// The bundle of the valid lanes of each aligned group of G lanes (G = 64: the whole packet); every
+// lane returns its own group's bundle.  All lanes must call (shuffles stay inside a group).
+template <int G>
+__device__ __forceinline__ Bundle make_bundle_g(const Lane &L, bool valid) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long m = __ballot(valid);
+    const unsigned long long gm = G == 64 ? m : ((m >> (lane & ~(G - 1))) & ((1ull << G) - 1ull));
+    const int cnt = __popcll(gm);
+    const float n = (float)(cnt > 0 ? cnt : 1);
     Bundle K;
-    const float n = (float)__popcll(__ballot(valid));
-    K.co = mk(wave_sum(valid ? L.o.x : 0.f) / n, wave_sum(valid ? L.o.y : 0.f) / n, wave_sum(valid ? L.o.z : 0.f) / n);
-    const f3 su = mk(wave_sum(valid ? L.au.x : 0.f), wave_sum(valid ? L.au.y : 0.f), wave_sum(valid ? L.au.z : 0.f));
+    K.co = mk(grp_sum<G>(valid ? L.o.x : 0.f) / n, grp_sum<G>(valid ? L.o.y : 0.f) / n,
+              grp_sum<G>(valid ? L.o.z : 0.f) / n);
+    const f3 su = mk(grp_sum<G>(valid ? L.au.x : 0.f), grp_sum<G>(valid ? L.au.y : 0.f), grp_sum<G>(valid ? L.au.z : 0.f));
     const float sl = sqrtf(lensq3(su));
-    K.omax = wave_max(valid ? L.omax : 0.f);
-    if (!(sl > 0.f) || !isfinite(sl)) {
-        K.cu = mk(0.f, 0.f, 1.f);
-        K.delta = FLT_MAX;
-        return K;
-    }
-    K.cu = mk(su.x / sl, su.y / sl, su.z / sl);
+    K.omax = grp_max<G>(valid ? L.omax : 0.f);
+    const bool ok = cnt > 0 && sl > 0.f && isfinite(sl);
+    K.cu = ok ? mk(su.x / sl, su.y / sl, su.z / sl) : mk(0.f, 0.f, 1.f);
     const auto perp = [&](f3 x) {
         const f3 t = sub3(x, K.co);
         const f3 c = mk(t.y * K.cu.z - t.z * K.cu.y, t.z * K.cu.x - t.x * K.cu.z, t.x * K.cu.y - t.y * K.cu.x);
@@ -412,8 +423,20 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
     };
     const float dl = valid ? fmaxf(perp(L.o), perp(L.p)) : 0.f;
     const float cm = fmaxf(fmaxf(fabsf(K.co.x), fabsf(K.co.y)), fabsf(K.co.z));
-    const float d = wave_max(dl);
-    K.delta = isfinite(d) ? d * 1.0001f + 1e-5f * (K.omax + cm) + 1e-6f : FLT_MAX;
+    const float d = grp_max<G>(dl);
+    K.delta = (ok && isfinite(d)) ? d * 1.0001f + 1e-5f * (K.omax + cm) + 1e-6f : FLT_MAX;
+    return K;
+}
+
+__device__ __forceinline__ float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
+// The whole packet's bundle, wave-uniform: kept in SGPRs.
+__device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
+    Bundle K = make_bundle_g<64>(L, valid);
+    K.co = mk(uniform_f(K.co.x), uniform_f(K.co.y), uniform_f(K.co.z));
+    K.cu = mk(uniform_f(K.cu.x), uniform_f(K.cu.y), uniform_f(K.cu.z));
+    K.delta = uniform_f(K.delta);
+    K.omax = uniform_f(K.omax);
     return K;
 }
 
