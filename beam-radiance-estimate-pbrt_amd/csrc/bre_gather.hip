@@ -936,7 +936,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, const Lane &M, int fi
 template <bool COUNT>
 __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, int first, int n,
                                                const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
-                                               float R, Prof &pf) {
+                                               float R, const float *__restrict__ sd, int64_t seg0, Prof &pf) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
     const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
@@ -951,9 +951,10 @@ __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, in
     bool hit = on & node_test(r.box, o, invs, tmax, te);
     const bool inf = __shfl((int)M.has_inf, sl) != 0;
     if (__ballot(on & inf) != 0ull) {
-        // shuffle with every lane active: ds_bpermute reads 0 from a lane outside EXEC
-        const f3 d = mk(lane_f(M.d.x, sl), lane_f(M.d.y, sl), lane_f(M.d.z, sl));
         if (on & inf) {
+            // the rare axis-parallel ray: its direction is re-read (keeps Lane::d out of registers)
+            const int64_t so = seg0 + sl;
+            const f3 d = mk(sd[3 * so], sd[3 * so + 1], sd[3 * so + 2]);
             const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
             hit = slab_test(r.box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
         }
@@ -1045,6 +1046,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     TileShared &sh = shm[w];
     const int64_t s = grp * kTileBlock + threadIdx.x;
+    const int64_t seg0 = grp * kTileBlock + (int64_t)__builtin_amdgcn_readfirstlane(w) * 64;  // lane 0 of this wave
     // behind kernel 3 (auto), only the packets it handed over run here; the test is per wave (one
     // packet), so a ragged last packet keeps all 64 lanes (tile staging and shuffles need them)
     if (redo) {
@@ -1138,7 +1140,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                     t1 += __popcll(m);
                     __builtin_amdgcn_wave_barrier();
                     if (t1 - h1 >= 64) {
-                        if (dbg != 2) tile_box_exact<COUNT>(sh, L, h1, 64, recs, pw, R, pf);
+                        if (dbg != 2) tile_box_exact<COUNT>(sh, L, h1, 64, recs, pw, R, sd, seg0, pf);
                         h1 += 64;
                         if (h1 >= 1024) {
                             h1 -= 1024;
@@ -1234,7 +1236,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
         if (dbg != 2 && t1 > h1) {
-            if (PFIRST) tile_box_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
+            if (PFIRST) tile_box_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, sd, seg0, pf);
             else tile_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
         }
         h1 = t1 = 0;
