@@ -182,7 +182,9 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = nvalid;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
-    const int K = c->leaf_size;
+    // auto (kernel 0) runs kernel 4 on one tree of leaf2-beam tiles
+    const int K = c->kernel == 0 ? c->leaf2 : c->leaf_size;
+    b.leaf_size = K;  // the hierarchy kernels size their work by it: must match the buffers below
     const int64_t nleaf = (nvalid + K - 1) / K;
     const int64_t nnodes = nleaf > 1 ? nleaf - 1 : 1;
     HIPCHK(c, c->recs.ensure((size_t)nvalid * sizeof(BeamRec)));
@@ -197,10 +199,10 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.visit = c->visit.as<unsigned int>();
     HIPCHK(c, launch_pack(b, nvalid, c->stream));
     HIPCHK(c, launch_hierarchy(b, nvalid, c->stream));
-    // auto mode: a second hierarchy over the same sorted beam records with leaf tiles of leaf2
-    // beams, for the packets kernel 3 hands over to kernel 4 (leaf_parent / visit are reused:
-    // the second tree has fewer leaves, and stream order serialises the two builds)
-    if (c->kernel == 0 && K <= kProxyMaxLeafHost && c->leaf2 > K) {
+    // hand-over mode (kernel 6): a second hierarchy over the same sorted beam records with leaf
+    // tiles of leaf2 beams, for the packets kernel 3 hands over to kernel 4 (leaf_parent / visit
+    // are reused: the second tree has fewer leaves, and stream order serialises the two builds)
+    if (c->kernel == 6 && K <= kProxyMaxLeafHost && c->leaf2 > K) {
         const int K2 = c->leaf2;
         const int64_t nleaf2 = (nvalid + K2 - 1) / K2;
         HIPCHK(c, c->nodes2.ensure((size_t)(nleaf2 > 1 ? nleaf2 - 1 : 1) * sizeof(Node)));
@@ -384,13 +386,13 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, launch_zero_outputs(a, c->stream));
         return BRE_OK;
     }
-    // auto (0): the packet-proxy kernel 3 (with kernel 1 as its device-side overflow fallback)
-    // when leaf clusters are small enough for its candidate list, else kernel 1
-    // auto (0): kernel 3 on the small-leaf tree with kernel 4 on the tile tree taking the packets it
-    // hands over; with leaf clusters too large for kernel 3, kernel 4 alone
+    // auto (0): kernel 4 on the tile tree.  Hand-over (6): kernel 3 on the small-leaf tree with
+    // kernel 4 on the tile tree taking the packets it hands over (launch_gather's mode 0); with
+    // leaf clusters too large for kernel 3, kernel 4 alone
     int kernel = c->kernel;
     if (kernel == 5) return gather_chunk(c, a);
-    if (kernel == 0 && c->built_leaf2 == 0) kernel = c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 4;
+    if (kernel == 0) kernel = 4;
+    else if (kernel == 6) kernel = c->built_leaf2 == 0 ? (c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 4) : 0;
     if (kernel == 3 && c->built_leaf_size > kProxyMaxLeafHost)
         return fail(c, BRE_ERR_STATE, "kernel 3 needs BRE_OPT_LEAF_SIZE <= %d", kProxyMaxLeafHost);
     if (kernel != 2) {
@@ -518,7 +520,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
     case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
     case BRE_OPT_KERNEL:
-        if (value < 0 || value > 5) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..5");
+        if (value < 0 || value > 6) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..6");
         c->kernel = (int)value;
         return BRE_OK;
     case BRE_OPT_LEAF_SIZE:

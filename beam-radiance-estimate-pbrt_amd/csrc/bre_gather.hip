@@ -633,7 +633,10 @@ __device__ __forceinline__ void proxy_batch_q(ProxyQ &q, const Lane &L, bool val
         }
         nk = __popcll(km);
     }
-    if (COUNT) pf.beams += nb;
+    if (COUNT) {
+        pf.beams += nb;
+        pf.useful += __popcll(__ballot(keep));  // beams kept by the bundle test
+    }
     __builtin_amdgcn_wave_barrier();
     int qh = 0, qt = 0;  // wave-uniform ring head / tail (the ring is drained per batch)
     for (int j = 0; j < nk; ++j) {
@@ -1113,6 +1116,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 }
                 unsigned long long todo = COUNT ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull))
                                                 : (km & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)));
+                if (COUNT) pf.useful += __popcll(km & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)));
                 while (todo != 0ull) {
                     const int j = __ffsll((long long)todo) - 1;
                     todo &= todo - 1ull;

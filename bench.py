@@ -112,10 +112,11 @@ ROOFLINE_REF = {
 }
 
 
-KERNEL_NAMES = {0: "auto (packet-proxy kernel 3 + leaf-tile kernel 4 hand-over)", 1: "depth-first wave-packet",
+KERNEL_NAMES = {0: "auto (kernel 4: leaf tiles of 64 beams, packet bundle reject, compacted pair queue)", 1: "depth-first wave-packet",
                 2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over",
                 4: "leaf tiles + wavefront-compacted pair queue",
-                5: "capsule-chunk index (contributing pairs only)"}
+                5: "capsule-chunk index (contributing pairs only)",
+                6: "hand-over (packet-proxy kernel 3 + leaf-tile kernel 4)"}
 
 
 def main():
@@ -237,6 +238,7 @@ def main():
         "max_stack_depth": st["max_stack_depth"],
         "redo_items": st["redo_items"],
         "prefilter_rejects_per_estimate": st["prefilter_rejects"] / nseg_d,
+        "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
         "chunks": st.get("n_chunks", 0),
     }
     result.update(diag)
@@ -259,7 +261,7 @@ def main():
             "V_ref_tree": v_ref,
             "C": c_ref,
             "V_C_source": source,
-            "kernel": "gather (k_gather_proxy + k_gather_tile hand-over)",
+            "kernel": "gather (k_gather_tile; k_gather_proxy too in hand-over mode)",
         }
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -298,8 +300,7 @@ def pmc_traffic(path):
             if "hbm_read_bytes_corrected" not in v:
                 continue
             tot += (v["hbm_read_bytes_corrected"] + v.get("hbm_write_bytes", 0.0)) * v["calls"]
-            if name.startswith("k_gather_proxy"):
-                calls += v["calls"]
+            calls = max(calls, v["calls"])  # every gather launches each of its kernels once
     return tot / calls if calls else None
 
 

@@ -63,13 +63,16 @@ typedef enum bre_status {
 typedef enum bre_option {
     BRE_OPT_COUNTERS = 1,    /* 0/1: per-segment candidate / contribution / node-visit counting */
     BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
-    BRE_OPT_KERNEL = 3,      /* 0 = auto: with leaf size <= 4, kernel 3 on that tree and kernel 4 on a
-                                second tree with BRE_OPT_TILE_LEAF-beam leaves (same beam records)
-                                for the packets kernel 3 hands over; larger leaves: kernel 4.
+    BRE_OPT_KERNEL = 3,      /* 0 = auto (default): kernel 4 on a tree of BRE_OPT_TILE_LEAF-beam leaf
+                                tiles, with the packet bundle reject (fastest measured at C2).
                                 1 = depth-first wave-packet traversal, 2 = thread-per-segment,
                                 3 = packet-proxy traversal with incoherent / overflowing packets
                                 handed to kernel 1 on the device, 4 = depth-first traversal over
-                                leaf tiles with wavefront-compacted pair queues */
+                                leaf tiles (BRE_OPT_LEAF_SIZE) with wavefront-compacted pair queues,
+                                5 = capsule-chunk index, 6 = hand-over: kernel 3 on the
+                                BRE_OPT_LEAF_SIZE (<= 4) tree, kernel 4 on a second tree of
+                                BRE_OPT_TILE_LEAF-beam tiles for the packets kernel 3 hands over.
+                                Every kernel gives the same pair contributions. */
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..64 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
     BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 8) */
@@ -80,13 +83,13 @@ typedef enum bre_option {
     BRE_OPT_SHARD_COUNT = 9, /* camera pass: number of image-tile shards (default 1 = all tiles).
                                 Set the count before the rank.  Per-pixel results do not depend on
                                 the sharding, so summing the shards' Ld gives the 1-shard image. */
-    BRE_OPT_TILE_LEAF = 10,  /* auto mode: beams per leaf tile of the hand-over tree, 1..64 (default
-                                32); applies at the next build */
+    BRE_OPT_TILE_LEAF = 10,  /* kernels 0 / 6: beams per leaf tile of the kernel-4 tree, 1..64
+                                (default 64); applies at the next build */
     BRE_OPT_CHUNK_LEN = 11,  /* kernel 5: chunk length in units of E/100, E = (R + r)(1 + 1e-3) + margin
                                 (25..100000, default 400) */
     BRE_OPT_CHUNK_LEAF = 12, /* kernel 5: chunks per LBVH leaf, 1..64 (default 1) */
     BRE_OPT_SORT_SEGMENTS = 13 /* bre_gather_camera: 0/1 hand the camera-pass segments to the gather
-                                  in 5-D Morton order of (origin, direction) (default 1); pixel sums
+                                  in 6-D Morton order of (origin, end point) (default 1); pixel sums
                                   are the same pair contributions either way */
 } bre_option;
 
@@ -104,7 +107,7 @@ typedef struct bre_stats {
     int64_t beam_evals;      /* kernel 1, counters: beam records evaluated, per wave */
     int64_t ccp_wave_evals;  /* kernel 1, counters: exact closest-point executions, per wave */
     int64_t prefilter_rejects; /* kernel 1, counters: lane-level line-distance rejects */
-    int64_t useful_beam_evals; /* kernel 1, counters: beam evaluations where >= 1 lane is a candidate */
+    int64_t useful_beam_evals; /* counters: kernel 1 beam evaluations where >= 1 lane is a candidate; kernels 3/4: beams kept by the packet bundle test */
     int64_t max_stack_depth;   /* kernel 3, counters: deepest LDS node stack used by any wave */
     int64_t redo_items;        /* kernel 3, counters: (packet, subtree) items handed to kernel 1
                                   (incoherent packets or LDS-stack overflow) */

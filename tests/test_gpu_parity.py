@@ -36,7 +36,7 @@ def ctxs(bre):
         c.close()
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 6])
 @pytest.mark.parametrize("leaf", [1, 4, 8, 64])
 def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     if kernel == 3 and leaf > 4:
@@ -56,7 +56,7 @@ def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     assert st["contributions"] == int(ref["contrib"].sum())
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 6])
 def test_bounce_segments_match_oracle(bre, synth, oracle, kernel):
     beams = synth.fog_beams(3000, seed=99)
     segs = synth.bounce_segments(3000, seed=5)
@@ -158,8 +158,9 @@ def test_axis_aligned_rays_and_degenerate_segments(bre, oracle):
     ref = oracle.build(beams).gather(segs, 0.02)
     with bre.BeamGather(0, counters=True) as g:
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        for k in (1, 2, 3):
-            g.set_option(bre.OPT_KERNEL, k)
+        for k in (0, 1, 2, 3, 4, 6):
+            g.set_option(bre.OPT_KERNEL, k)  # the tree shape follows the kernel: rebuild
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
             out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
             assert np.array_equal(out["counts"][:, 0], ref["cand"]), k
             assert np.array_equal(out["counts"][:, 1], ref["contrib"]), k
@@ -224,7 +225,7 @@ def test_deterministic_per_segment(bre, synth):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 3, 4])
+@pytest.mark.parametrize("kernel", [0, 1, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 2, 8, 64])
 def test_subtree_split_matches_oracle(bre, synth, oracle, split, kernel):
     beams = synth.fog_beams(4000, seed=51)
@@ -310,8 +311,9 @@ def test_kernel3_stack_overflow_falls_back_exactly(bre, synth, oracle):
 
 @pytest.mark.parametrize("tile_leaf", [8, 32, 64])
 def test_auto_handover_mixed_packets(bre, synth, oracle, tile_leaf):
-    """Auto mode: coherent camera packets stay in kernel 3, incoherent bounce packets go to kernel 4
-    on the tile tree; one gather over both kinds matches the oracle exactly (sets) and to rounding."""
+    """Hand-over mode (kernel 6): coherent camera packets stay in kernel 3, incoherent bounce packets
+    go to kernel 4 on the tile tree; one gather over both kinds matches the oracle exactly (sets) and
+    to rounding."""
     beams = synth.fog_beams(6000, seed=81, mean_length=0.4)
     cam = synth.camera_segments(32, 32, seed=82)
     bnc = synth.bounce_segments(2048, seed=83, npix=1024)
@@ -319,7 +321,7 @@ def test_auto_handover_mixed_packets(bre, synth, oracle, tile_leaf):
     R = 0.012
     ref = oracle.build(beams).gather(segs, R, npix=1024)
     accum = np.zeros((1024, 3), np.float32)
-    with bre.BeamGather(0, counters=True, kernel=0) as g:
+    with bre.BeamGather(0, counters=True, kernel=6) as g:
         g.set_option(bre.OPT_TILE_LEAF, tile_leaf)
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
         out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, npix=1024, accum=accum,
