@@ -963,6 +963,8 @@ __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, in
         }
     }
     if (__ballot(hit) == 0ull) return;
+    // the power load is issued ahead of the closest-point arithmetic (most box hits contribute)
+    const float4 pv = hit ? pw[b] : make_float4(0.f, 0.f, 0.f, 0.f);
     const f3 p = mk(lane_f(M.p.x, sl), lane_f(M.p.y, sl), lane_f(M.p.z, sl));
     const f3 au = mk(lane_f(M.au.x, sl), lane_f(M.au.y, sl), lane_f(M.au.z, sl));
     const float mag_a = lane_f(M.mag_a, sl);
@@ -973,7 +975,6 @@ __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, in
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
             const float w = sqrtf(1.0f - rr * rr);
-            const float4 pv = pw[b];
             atomicAdd(&sh.acc[0][sl], pv.x * w);
             atomicAdd(&sh.acc[1][sl], pv.y * w);
             atomicAdd(&sh.acc[2][sl], pv.z * w);
@@ -1503,6 +1504,8 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     do {                                           \
         if (a.tile_mode == 1 && a.occupancy >= 8)  \
             BRE_LAUNCH_TILE_W(C, P, 8, true);      \
+        else if (a.tile_mode == 1 && a.occupancy == 7) \
+            BRE_LAUNCH_TILE_W(C, P, 7, true);      \
         else if (a.tile_mode == 1)                 \
             BRE_LAUNCH_TILE_W(C, P, 1, true);      \
         else if (a.occupancy >= 8)                 \
