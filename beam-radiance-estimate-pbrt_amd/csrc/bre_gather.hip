@@ -884,6 +884,43 @@ __global__ __launch_bounds__(64, MINW) void k_gather_proxy(
 //      the segment's LDS accumulator.
 // Same per-pair arithmetic as kernel 1; only the float summation order of a segment's
 // contributions differs (deterministic: queue order is fixed by the traversal).
+// Kernel 4's per-lane prefilter in separable form.  With t = b0 - o and n = au x bu,
+//   t.n = au.(bu x b0) - bu.(o x au) = au.m0 - bu.q,
+// so per (lane, beam) only two dot products and c = au.bu remain: m0 is staged per beam, q per lane.
+// |n|^2 = |au|^2|bu|^2 - c^2 (Lagrange) is bracketed by 0.99999 - c^2 <= |n|^2 <= 1.00001 - c^2
+// (unit vectors to ~1e-7, c to ~5e-7).  The computed t.n is within 1e-5 (bmax + omax) + 1e-6 of
+// the exact one (~2e-6 (bmax + omax) by the float error of the cross and dot products), and the
+// coordinate bound mag of far_from_lines uses tl <= |b0|_1 + |o|_1, so its margins split into a
+// beam part (staged: Ab, Eb) and a lane part (Al, El):
+//   reject  <=>  tn > (Eb + El) + (Ab + Al) * (sqrt(nn_hi) * 1.000001 + 1e-6)
+// which implies the line-line distance exceeds maxd * 1.0001 + 2 eps with eps >= far_from_lines'
+// eps: the same proof that every reference-computed distance of the pair is >= maxd.  Near-parallel
+// pairs (|n|^2 possibly < 1e-2) and zero-length segments (El = FLT_MAX) are never rejected.
+struct ScanLane {
+    f3 q;       // o x au
+    float al;   // 2e-5 (omax + 10 |o|_1)
+    float el;   // 1e-5 omax, FLT_MAX for a zero-length segment
+};
+
+__device__ __forceinline__ ScanLane make_scan_lane(const Lane &L) {
+    ScanLane S;
+    S.q = mk(L.o.y * L.au.z - L.o.z * L.au.y, L.o.z * L.au.x - L.o.x * L.au.z, L.o.x * L.au.y - L.o.y * L.au.x);
+    const float o1 = fabsf(L.o.x) + fabsf(L.o.y) + fabsf(L.o.z);
+    S.al = 2e-5f * (L.omax + 10.0f * o1);
+    S.el = L.mag_a == 0.0f ? FLT_MAX : 1e-5f * L.omax;
+    return S;
+}
+
+__device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, f3 bu, f3 m0, float ab, float eb) {
+    const float c = __builtin_fmaf(au.x, bu.x, __builtin_fmaf(au.y, bu.y, au.z * bu.z));
+    const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
+    if (!(nn_lo >= 1e-2f)) return false;
+    const float x = __builtin_fmaf(au.x, m0.x, __builtin_fmaf(au.y, m0.y, au.z * m0.z));
+    const float tn = fabsf(__builtin_fmaf(-bu.x, S.q.x, __builtin_fmaf(-bu.y, S.q.y, __builtin_fmaf(-bu.z, S.q.z, x))));
+    const float nl = __builtin_amdgcn_sqrtf(__builtin_fmaf(-c, c, 1.00001f)) * 1.000001f + 1e-6f;
+    return tn > __builtin_fmaf(ab + S.al, nl, eb + S.el);
+}
+
 constexpr int kTileBlock = 256;  // 4 waves
 constexpr int kQueueCap = 128;   // >= 63 left over + 64 appended by one beam / one flush
 constexpr int kTileMax = 32;     // beams staged in LDS at a time (longer leaves go in chunks; 64 costs occupancy)
@@ -1062,6 +1099,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     Bundle K;
     K.delta = FLT_MAX;
     if (PFIRST && PREF && __ballot(valid) != 0ull) K = make_bundle(L, valid);
+    const ScanLane SL = PFIRST ? make_scan_lane(L) : ScanLane{};
     sh.acc[0][lane] = 0.f;
     sh.acc[1][lane] = 0.f;
     sh.acc[2][lane] = 0.f;
@@ -1087,7 +1125,23 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int nb = min(kTileMax, cnt - base);
             const int64_t tile0 = first + base;
             __builtin_amdgcn_wave_barrier();
-            {
+            if (PFIRST) {
+                // lane j stages beam j in the scan layout (see ScanLane): (b0, maxd), (bu, Ab),
+                // (m0 = bu x b0, Eb); the exact stage reads the beam record itself from L2
+                if (lane < nb) {
+                    const BeamV r = load_beam(recs, tile0 + lane);
+                    const float maxd = R + r.radius;
+                    const f3 m0 = mk(r.bu.y * r.b0.z - r.bu.z * r.b0.y, r.bu.z * r.b0.x - r.bu.x * r.b0.z,
+                                     r.bu.x * r.b0.y - r.bu.y * r.b0.x);
+                    const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
+                    const float b1 = fabsf(r.b0.x) + fabsf(r.b0.y) + fabsf(r.b0.z);
+                    const float ab = maxd * 1.0001f + 2e-5f * (bmax + 10.0f * b1) + 2e-6f;
+                    const float eb = 1e-5f * bmax + 1e-6f;
+                    sh.tile[lane][0] = make_float4(r.b0.x, r.b0.y, r.b0.z, maxd);
+                    sh.tile[lane][1] = make_float4(r.bu.x, r.bu.y, r.bu.z, ab);
+                    sh.tile[lane][2] = make_float4(m0.x, m0.y, m0.z, eb);
+                }
+            } else {
                 // 64 lanes copy nb lines of 4 x 16 B: item r -> (beam r >> 1, half r & 1)
                 for (int r = lane; r < 2 * nb; r += 64) {
                     const int bj = r >> 1, h = (r & 1) * 2;
@@ -1110,8 +1164,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 if (PREF) {
                     bool keep = false;
                     if (lane < nb) {
-                        const float4 y = sh.tile[lane][1], z = sh.tile[lane][2], wv = sh.tile[lane][3];
-                        keep = !bundle_far(K, mk(y.z, y.w, z.x), mk(z.y, z.z, z.w), R + wv.y);
+                        const float4 x = sh.tile[lane][0], y = sh.tile[lane][1];
+                        keep = !bundle_far(K, mk(x.x, x.y, x.z), mk(y.x, y.y, y.z), x.w);
                     }
                     km = __ballot(keep);
                 }
@@ -1121,14 +1175,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 while (todo != 0ull) {
                     const int j = __ffsll((long long)todo) - 1;
                     todo &= todo - 1ull;
-                    const float4 y = sh.tile[j][1], z = sh.tile[j][2], wv = sh.tile[j][3];
                     bool need = lane_on && ((km >> j) & 1ull);
-                    if (PREF)
-                        need = need && !far_from_lines_fast(L.o, L.au, L.mag_a, L.omax, mk(y.z, y.w, z.x),
-                                                            mk(z.y, z.z, z.w), R + wv.y);
+                    if (PREF) {
+                        const float4 y = sh.tile[j][1], z = sh.tile[j][2];
+                        need = need && !scan_far(SL, L.au, mk(y.x, y.y, y.z), mk(z.x, z.y, z.z), y.w, z.w);
+                    }
                     if (COUNT) {
-                        const float4 x = sh.tile[j][0];
-                        const Box6 box{x.x, x.y, x.z, x.w, y.x, y.y};
+                        const Box6 box = load_beam(recs, tile0 + j).box;
                         float te;
                         bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                         if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);

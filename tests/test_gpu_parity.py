@@ -252,7 +252,7 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         segs = synth.camera_segments(64, 64, seed=64) if kind == "camera" else synth.bounce_segments(4096, seed=65)
         R = 0.01
     outs = []
-    for k, pf in ((1, False), (1, True), (3, False), (3, True), (4, False), (4, True)):
+    for k, pf in ((1, False), (1, True), (3, False), (3, True), (4, False), (4, True), (0, False), (0, True)):
         with bre.BeamGather(0, counters=True, kernel=k, prefilter=pf) as g:
             g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
             outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True))
@@ -264,6 +264,45 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         assert _seg_close(o["seg_rgb"], outs[0]["seg_rgb"]) <= SEG_RTOL
     assert np.array_equal(outs[2]["seg_rgb"], outs[3]["seg_rgb"])
     assert np.array_equal(outs[4]["seg_rgb"], outs[5]["seg_rgb"])
+    assert np.array_equal(outs[6]["seg_rgb"], outs[7]["seg_rgb"])
+
+
+@pytest.mark.parametrize("offset", [0.0, 37.5, -250.0])
+def test_prefilters_at_the_threshold(bre, oracle, offset):
+    """Beams whose line passes at distance (R + r)(1 + e) of a segment, e in [-1e-3, 1e-3], at
+    coordinates far from the origin: the packet bundle test and the separable per-lane prefilter
+    may only drop pairs the reference computes as d >= R + r (exact contribution sets)."""
+    rng = np.random.default_rng(int(abs(offset)) + 3)
+    R, r = np.float32(0.02), np.float32(0.01)
+    n = 4096
+    base = np.float32(offset) + rng.random((n, 3), np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    seg_len = np.float32(0.5)
+    o = base.astype(np.float32)
+    p = (o + d * seg_len).astype(np.float32)
+    # beam: direction e perpendicular to d, through a point at distance (R + r)(1 + eps) from the
+    # segment's midpoint along a third direction perpendicular to both
+    e = np.cross(d, rng.normal(size=(n, 3))).astype(np.float32)
+    e /= np.linalg.norm(e, axis=1, keepdims=True)
+    f = np.cross(d, e).astype(np.float32)
+    eps = rng.uniform(-1e-3, 1e-3, n).astype(np.float32)
+    mid = (o + d * (seg_len / 2)).astype(np.float32)
+    c = (mid + f * ((R + r) * (1 + eps))[:, None]).astype(np.float32)
+    start = (c - e * np.float32(0.3)).astype(np.float32)
+    end = (c + e * np.float32(0.3)).astype(np.float32)
+    beams = {"start": start, "end": end, "radius": np.full(n, r, np.float32),
+             "power": rng.random((n, 3), np.float32)}
+    segs = {"o": o, "p": p, "d": d, "tmax": np.full(n, seg_len, np.float32)}
+    ref = oracle.build(beams).gather(segs, float(R))
+    assert 0 < ref["contrib"].sum() < ref["cand"].sum()  # both sides of the threshold occur
+    for k in (0, 4):
+        with bre.BeamGather(0, counters=True, kernel=k) as g:
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=float(R), counts=True)
+        assert np.array_equal(out["counts"][:, 0], ref["cand"]), k
+        assert np.array_equal(out["counts"][:, 1], ref["contrib"]), k
+        assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
 
 
 @pytest.mark.parametrize("leaf", [16, 64])
