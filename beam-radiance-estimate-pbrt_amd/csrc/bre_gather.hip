@@ -1172,24 +1172,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 unsigned long long todo = COUNT ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull))
                                                 : (km & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)));
                 if (COUNT) pf.useful += __popcll(km & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)));
-                while (todo != 0ull) {
-                    const int j = __ffsll((long long)todo) - 1;
-                    todo &= todo - 1ull;
-                    bool need = lane_on && ((km >> j) & 1ull);
-                    if (PREF) {
-                        const float4 y = sh.tile[j][1], z = sh.tile[j][2];
-                        need = need && !scan_far(SL, L.au, mk(y.x, y.y, y.z), mk(z.x, z.y, z.z), y.w, z.w);
-                    }
-                    if (COUNT) {
-                        const Box6 box = load_beam(recs, tile0 + j).box;
-                        float te;
-                        bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
-                        if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
-                        cand += hit;
-                        pf.rejects += hit & !need;
-                    }
+                // queue the (beam, lane) survivors of beam j; drain 64 at a time (ring < 128)
+                const auto push = [&](int j, bool need) {
                     const unsigned long long m = __ballot(need);
-                    if (m == 0ull) continue;
+                    if (m == 0ull) return;
                     if (need) {
                         const int pos = (t1 + lanes_below(m)) & (kQueueCap - 1);
                         sh.qb1[pos] = (int32_t)(tile0 + j);
@@ -1206,6 +1192,43 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                         }
                         __builtin_amdgcn_wave_barrier();
                     }
+                };
+                if (!COUNT && PREF) {
+                    // two kept beams per step: independent LDS reads and prefilters (ILP), then the
+                    // survivors are queued beam by beam in order
+                    while (todo != 0ull) {
+                        const int j1 = __ffsll((long long)todo) - 1;
+                        todo &= todo - 1ull;
+                        const bool two = todo != 0ull;
+                        const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
+                        if (two) todo &= todo - 1ull;
+                        const float4 y1 = sh.tile[j1][1], z1 = sh.tile[j1][2];
+                        const float4 y2 = sh.tile[j2][1], z2 = sh.tile[j2][2];
+                        const bool n1 = lane_on && !scan_far(SL, L.au, mk(y1.x, y1.y, y1.z), mk(z1.x, z1.y, z1.z), y1.w, z1.w);
+                        const bool n2 = two && lane_on &&
+                                        !scan_far(SL, L.au, mk(y2.x, y2.y, y2.z), mk(z2.x, z2.y, z2.z), y2.w, z2.w);
+                        push(j1, n1);
+                        if (two) push(j2, n2);
+                    }
+                    continue;
+                }
+                while (todo != 0ull) {
+                    const int j = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1ull;
+                    bool need = lane_on && ((km >> j) & 1ull);
+                    if (PREF) {
+                        const float4 y = sh.tile[j][1], z = sh.tile[j][2];
+                        need = need && !scan_far(SL, L.au, mk(y.x, y.y, y.z), mk(z.x, z.y, z.z), y.w, z.w);
+                    }
+                    if (COUNT) {
+                        const Box6 box = load_beam(recs, tile0 + j).box;
+                        float te;
+                        bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
+                        if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
+                        cand += hit;
+                        pf.rejects += hit & !need;
+                    }
+                    push(j, need);
                 }
                 continue;
             }
