@@ -39,16 +39,18 @@ __global__ void k_sort_init(unsigned int *b) {
 
 __global__ __launch_bounds__(kBlock) void k_origin_bounds(int64_t n, const float *__restrict__ o,
                                                           unsigned int *__restrict__ b) {
-    // (key mode 1 launches it twice, over the origins and the end points, into one box)
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    // (key mode 1 launches it twice, over the origins and the end points, into one box).
+    // Grid-stride with a block reduction: one set of 6 atomics per block, not per wave.
+    __shared__ unsigned int red[kBlock / 64][6];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
-    bool any = false;
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         const float v[3] = {o[3 * i], o[3 * i + 1], o[3 * i + 2]};
         if (isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2])) {
-            any = true;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) mn[k] = mx[k] = f2ord(v[k]);
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = min(mn[k], f2ord(v[k]));
+                mx[k] = max(mx[k], f2ord(v[k]));
+            }
         }
     }
 #pragma unroll
@@ -59,11 +61,29 @@ __global__ __launch_bounds__(kBlock) void k_origin_bounds(int64_t n, const float
             mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
         }
     }
-    if ((threadIdx.x & 63) == 0 && __ballot(any) != 0ull) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            atomicMin(&b[k], mn[k]);
-            atomicMax(&b[3 + k], mx[k]);
+            red[w][k] = mn[k];
+            red[w][3 + k] = mx[k];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < kBlock / 64; ++v) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = min(mn[k], red[v][k]);
+                mx[k] = max(mx[k], red[v][3 + k]);
+            }
+        }
+        if (mn[0] <= mx[0]) {  // at least one finite point
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                atomicMin(&b[k], mn[k]);
+                atomicMax(&b[3 + k], mx[k]);
+            }
         }
     }
 }
@@ -173,9 +193,10 @@ size_t seg_sort_temp_bytes(int64_t n) {
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     if (s.n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sort_init, dim3(1), dim3(64), 0, st, s.bounds);
-    hipLaunchKernelGGL(k_origin_bounds, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
+    const unsigned bgrid = grid_of(s.n) < 1024u ? grid_of(s.n) : 1024u;  // grid-stride bounds
+    hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
     if (s.key_mode == 1) {
-        hipLaunchKernelGGL(k_origin_bounds, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
+        hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
         hipLaunchKernelGGL(k_seg_keys_op, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.bounds, s.keys,
                            s.vals);
     } else {

@@ -11,5 +11,5 @@ i=0
 for a in "$@"; do
   i=$((i+1))
   timeout -k 10 300 python -u bench.py ${STEPS:---steps 3 --warmup 1} --no-cpu $a > "$OUT/bench$i.log" 2>&1 || { tail -n 20 "$OUT/bench$i.log"; exit 1; }
-  echo "[$a] $(grep '^{' "$OUT/bench$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print({k: round(d.get(k),1) for k in ("value","ms_per_step","gather_kernel_ms","contributions_per_estimate","bundle_keep_frac","beam_evals_per_wave") if d.get(k) is not None})')"
+  echo "[$a] $(grep '^{' "$OUT/bench$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print({k: round(d.get(k),1) for k in ("value","ms_per_step","gather_kernel_ms","contributions_per_estimate","bundle_keep_frac","bvh_build_ms","photon_pass_ms") if d.get(k) is not None})')"
 done
