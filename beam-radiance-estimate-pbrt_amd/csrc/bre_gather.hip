@@ -976,7 +976,8 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, const Lane &M, int fi
 template <bool COUNT>
 __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, int first, int n,
                                                const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
-                                               float R, const float *__restrict__ sd, int64_t seg0, Prof &pf) {
+                                               float R, const float *__restrict__ sd, int64_t seg0, Prof &pf,
+                                               int dbg = 0) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
     const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
@@ -1000,6 +1001,10 @@ __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, in
         }
     }
     if (__ballot(hit) == 0ull) return;
+    if (dbg == 3) {  // timing-only: queue, shuffles, beam load and box test, no closest points
+        if (hit) atomicAdd(&sh.acc[0][sl], r.radius);
+        return;
+    }
     // the power load is issued ahead of the closest-point arithmetic (most box hits contribute)
     const float4 pv = hit ? pw[b] : make_float4(0.f, 0.f, 0.f, 0.f);
     const f3 p = mk(lane_f(M.p.x, sl), lane_f(M.p.y, sl), lane_f(M.p.z, sl));
@@ -1184,7 +1189,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                     t1 += __popcll(m);
                     __builtin_amdgcn_wave_barrier();
                     if (t1 - h1 >= 64) {
-                        if (dbg != 2) tile_box_exact<COUNT>(sh, L, h1, 64, recs, pw, R, sd, seg0, pf);
+                        if (dbg != 2) tile_box_exact<COUNT>(sh, L, h1, 64, recs, pw, R, sd, seg0, pf, dbg);
                         h1 += 64;
                         if (h1 >= 1024) {
                             h1 -= 1024;
@@ -1317,7 +1322,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
         if (dbg != 2 && t1 > h1) {
-            if (PFIRST) tile_box_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, sd, seg0, pf);
+            if (PFIRST) tile_box_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, sd, seg0, pf, dbg);
             else tile_exact<COUNT>(sh, L, h1, t1 - h1, recs, pw, R, pf);
         }
         h1 = t1 = 0;
