@@ -249,13 +249,18 @@ def main():
         bytes_per_est = 32 + 12 + 32 * v_ref + 40 * c_ref
         per_launch = bytes_per_est * wl.segments_per_gather()
         achieved = per_launch / (gather_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.profile_summary or wl.default_profile())
         return {
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": pmc_traffic(args.profile_summary or wl.default_profile()),
+            "traffic": traffic,
+            # the PMC-measured bytes per launch over this run's launch time: the HBM/fabric
+            # bandwidth the kernel actually draws (the profile's launches average the same command)
+            "traffic_GBps": traffic / (gather_ms * 1e-3) / 1e9 if traffic else None,
+            "traffic_frac": traffic / (gather_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if traffic else None,
             "algorithmic_bytes_per_launch": per_launch,
             "bytes_per_estimate": bytes_per_est,
             "V_ref_tree": v_ref,
