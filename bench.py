@@ -104,11 +104,11 @@ WORKLOADS = {
 
 
 # V (reference-tree node tests) and C (candidates) per estimate of each workload's iteration 0,
-# measured by the oracle at N=1 (bench.py's CPU leg, profiles/r08/bench.json); used for the
+# measured by the oracle at N=1 (bench.py's CPU leg, profiles/r09/bench.json); used for the
 # roofline fields when this run has no CPU leg.  The beams and segments do not depend on N.
 ROOFLINE_REF = {
-    "c2": {"V_ref_tree": 1365328.295194508, "C": 420594.1388253242,
-           "source": "profiles/r08/bench.json (oracle SAH tree, CPU sample of iteration 0)"},
+    "c2": {"V_ref_tree": 1365412.6795491143, "C": 420520.3309178744,
+           "source": "profiles/r09/bench.json (oracle SAH tree, CPU sample of iteration 0)"},
 }
 
 
@@ -382,7 +382,7 @@ class SceneWorkload:
     def default_profile(self):
         if self.name != "c2":
             return None
-        return os.path.join(ROOT, "profiles", "r08", "profile_summary.json")
+        return os.path.join(ROOT, "profiles", "r09", "profile_summary.json")
 
     def config(self):
         a = self.args
