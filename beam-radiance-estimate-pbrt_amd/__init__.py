@@ -32,7 +32,8 @@ EXPORTS = [
     "bre_set_stream", "bre_synchronize", "bre_get_stats", "bre_set_beams",
     "bre_set_beams_device", "bre_gather", "bre_gather_device", "bre_beam_radius_at",
     "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell", "bre_scene_cornell_smoke", "bre_smoke_density",
-    "bre_camera_pass", "bre_gather_camera", "bre_get_segments", "bre_render_iteration", "bre_render",
+    "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
+    "bre_render_iteration", "bre_render",
     "bre_render_progressive",
 ]
 
@@ -122,6 +123,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_camera_pass.restype = I32
     lib.bre_gather_camera.argtypes = [P, F, P]
     lib.bre_gather_camera.restype = I32
+    lib.bre_gather_camera_segments.argtypes = [P, F, P, P, P]
+    lib.bre_gather_camera_segments.restype = I32
     lib.bre_get_segments.argtypes = [P, I64, P, P, P, P, P, P, ctypes.POINTER(I64)]
     lib.bre_get_segments.restype = I32
     lib.bre_render_iteration.argtypes = [P, P, P, I32, P]
@@ -246,6 +249,11 @@ class BeamGather:
     def gather_camera(self, R: float, accum):
         """Gather the last camera pass's segments into `accum` (torch CUDA tensor (W*H, 3))."""
         self._check(self.lib.bre_gather_camera(self.h, float(R), _ptr(accum)))
+
+    def gather_camera_segments(self, R: float, accum=None, seg_rgb=None, counts=None):
+        """bre_gather_camera with per-segment outputs (torch CUDA tensors, camera-pass order):
+        seg_rgb (n, 3) float32, counts (n, 2) int32 ({C or -1, contributions})."""
+        self._check(self.lib.bre_gather_camera_segments(self.h, float(R), _ptr(accum), _ptr(seg_rgb), _ptr(counts)))
 
     def get_segments(self):
         n = ctypes.c_int64(0)

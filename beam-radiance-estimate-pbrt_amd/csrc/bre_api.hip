@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -58,18 +59,13 @@ struct bre_ctx {
     int sqrt_mode = 0;
     int split = 8;
     bool prefilter = true;
-    int debug_mode = 0;
-    int stack_limit = 0;
-    int occupancy = 8;       // kernel 4 register budget (min waves per SIMD): 8 measured best at C2
+    int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
+    int occupancy = 8;       // tile kernel register budget (min waves per SIMD): 8 measured best at C2
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
-    int tile_mode = 1;       // kernel 4: prefilter-first leaf scan (1) or box-first (0)
-    float loose_cos = 0.f;
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
-    int leaf2 = 64;          // auto mode: leaf size of the tile tree kernel 4 takes hand-overs on (64 best at C2)
-    int built_leaf2 = 0;     // 0: no tile tree for the current beam set
-    int roots2_split = -1;
-    DevMem nodes2, roots2;
+    int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
+    unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
     int chunk_len = 400;   // chunk length in units of E / 100
     int chunk_leaf = 1;    // chunks per LBVH leaf
@@ -87,7 +83,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial, pcnt, redo;
+    DevMem counters_buf, roots, partial, pcnt;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // camera pass
@@ -134,8 +130,6 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = 0;
     c->nnodes = 0;
     c->roots_split = -1;
-    c->roots2_split = -1;
-    c->built_leaf2 = 0;
     c->stats = bre_stats{};
     c->stats.n_beams = n;
     if (n == 0) return BRE_OK;
@@ -182,7 +176,8 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = nvalid;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
-    // auto (kernel 0) runs kernel 4 on one tree of leaf2-beam tiles
+    // kernel 0 runs the tile kernel on one tree of leaf2-beam tiles; kernels 2 / 4 / 5 on a tree of
+    // BRE_OPT_LEAF_SIZE-beam leaves
     const int K = c->kernel == 0 ? c->leaf2 : c->leaf_size;
     b.leaf_size = K;  // the hierarchy kernels size their work by it: must match the buffers below
     const int64_t nleaf = (nvalid + K - 1) / K;
@@ -197,21 +192,11 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.nodes = c->nodes.as<Node>();
     b.leaf_parent = c->leaf_parent.as<int32_t>();
     b.visit = c->visit.as<unsigned int>();
+    b.nodes_cap = c->nodes.cap / sizeof(Node);
+    b.leaf_parent_cap = c->leaf_parent.cap / sizeof(int32_t);
+    b.visit_cap = c->visit.cap / sizeof(unsigned int);
     HIPCHK(c, launch_pack(b, nvalid, c->stream));
     HIPCHK(c, launch_hierarchy(b, nvalid, c->stream));
-    // hand-over mode (kernel 6): a second hierarchy over the same sorted beam records with leaf
-    // tiles of leaf2 beams, for the packets kernel 3 hands over to kernel 4 (leaf_parent / visit
-    // are reused: the second tree has fewer leaves, and stream order serialises the two builds)
-    if (c->kernel == 6 && K <= kProxyMaxLeafHost && c->leaf2 > K) {
-        const int K2 = c->leaf2;
-        const int64_t nleaf2 = (nvalid + K2 - 1) / K2;
-        HIPCHK(c, c->nodes2.ensure((size_t)(nleaf2 > 1 ? nleaf2 - 1 : 1) * sizeof(Node)));
-        BuildBuffers b2 = b;
-        b2.leaf_size = K2;
-        b2.nodes = c->nodes2.as<Node>();
-        HIPCHK(c, launch_hierarchy(b2, nvalid, c->stream));
-        c->built_leaf2 = K2;
-    }
     if (c->timing) {
         HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
         HIPCHK(c, hipEventSynchronize(c->ev[1]));
@@ -226,6 +211,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
 }
 
 bre_status read_counters(bre_ctx *c, DevCounters *ctr);
+bre_status check_flags(bre_ctx *c);
 
 // Kernel 5: build the capsule-chunk index for this gather's segments and R, then gather through it
 // (bre_chunk.hip).  Every array is a context buffer reused across calls; the beam build's sort
@@ -304,6 +290,9 @@ bre_status gather_chunk(bre_ctx *c, const GatherArgs &a) {
     bb.visit = c->visit.as<unsigned int>();
     bb.recs = reinterpret_cast<BeamRec *>(c->ch_recs.as<ChunkRec>());  // same leading lo / hi layout
     bb.nodes = c->ch_nodes.as<Node>();
+    bb.nodes_cap = c->ch_nodes.cap / sizeof(Node);
+    bb.leaf_parent_cap = c->leaf_parent.cap / sizeof(int32_t);
+    bb.visit_cap = c->visit.cap / sizeof(unsigned int);
     HIPCHK(c, launch_morton(bb, c->stream));
     HIPCHK(c, launch_sort(bb, c->stream));
     HIPCHK(c, launch_chunk_pack(cb, total, bb.vals_alt, bb.box, c->ch_slo.as<float>(), c->ch_shi.as<float>(),
@@ -336,19 +325,55 @@ bre_status gather_chunk(bre_ctx *c, const GatherArgs &a) {
     return read_counters(c, a.ctr);
 }
 
+// The counter block of the context: zeroed once at allocation; per gather only the counters are
+// zeroed, the sticky `flags` word stays until check_flags has read it.
+bre_status counters_block(bre_ctx *c, DevCounters **out) {
+    if (!c->counters_buf.ptr) {
+        HIPCHK(c, c->counters_buf.ensure(sizeof(DevCounters)));
+        HIPCHK(c, hipMemsetAsync(c->counters_buf.ptr, 0, sizeof(DevCounters), c->stream));
+    }
+    *out = c->counters_buf.as<DevCounters>();
+    HIPCHK(c, hipMemsetAsync(*out, 0, offsetof(DevCounters, flags), c->stream));
+    return BRE_OK;
+}
+
+// Synchronise the stream and turn the device's sticky error flags into a status (then clear them).
+// Every synchronising entry point ends here, so a traversal-stack overflow or a bad pixel index of
+// an earlier asynchronous gather is reported whatever the counters option (never silent).
+bre_status check_flags(bre_ctx *c) {
+    if (!c->counters_buf.ptr) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return BRE_OK;
+    }
+    if (!c->flags_host) {
+        void *h = nullptr;
+        HIPCHK(c, hipHostMalloc(&h, sizeof(unsigned int), hipHostMallocDefault));
+        c->flags_host = static_cast<unsigned int *>(h);
+    }
+    unsigned int *dflags = &c->counters_buf.as<DevCounters>()->flags;
+    HIPCHK(c, hipMemcpyAsync(c->flags_host, dflags, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const unsigned int f = *c->flags_host;
+    if (f == 0) return BRE_OK;
+    HIPCHK(c, hipMemsetAsync(dflags, 0, sizeof(unsigned int), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (f & kFlagStack)
+        return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than the stack): contributions "
+                    "were dropped");
+    return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix): segments were skipped");
+}
+
 bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
                          const int32_t *pixel, float R, int64_t npix, float *accum, float *seg_rgb,
-                         int32_t *seg_counts) {
+                         int32_t *seg_counts, const int32_t *seg_index = nullptr) {
     if (nseg < 0 || npix < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: negative size");
     if (nseg > 0 && (!o || !p || !d || !tmax))
         return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: null segment array");
     if (accum && !pixel) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: accum_rgb given without seg_pixel");
-    if (seg_counts && !c->counters)
-        return fail(c, BRE_ERR_STATE, "bre_gather: seg_counts needs BRE_OPT_COUNTERS=1");
-    HIPCHK(c, c->counters_buf.ensure(sizeof(DevCounters)));
-    DevCounters *ctr = c->counters_buf.as<DevCounters>();
-    HIPCHK(c, hipMemsetAsync(ctr, 0, sizeof(DevCounters), c->stream));
-    GatherArgs a;
+    DevCounters *ctr = nullptr;
+    bre_status st = counters_block(c, &ctr);
+    if (st != BRE_OK) return st;
+    GatherArgs a{};
     a.nseg = nseg;
     a.o = o;
     a.p = p;
@@ -360,6 +385,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.accum = accum;
     a.seg_rgb = seg_rgb;
     a.seg_counts = seg_counts;
+    a.seg_index = seg_index;
     a.recs = c->recs.as<BeamRec>();
     a.pow = c->pow.as<float4>();
     a.nodes = c->nodes.as<Node>();
@@ -368,34 +394,21 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.ctr = ctr;
     a.split = c->split;
     a.prefilter = c->prefilter;
-    a.debug_mode = c->debug_mode;
-    a.stack_limit = c->stack_limit;
     a.occupancy = c->occupancy;
-    a.tile_mode = c->tile_mode;
-    a.loose_cos = c->loose_cos;
-    a.roots = nullptr;
-    a.partial = nullptr;
-    a.pcnt = nullptr;
-    a.redo = nullptr;
-    a.nodes2 = nullptr;
-    a.roots2 = nullptr;
-    a.leaf2 = c->built_leaf2;
+    a.stack_cap = c->stack_cap;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
         HIPCHK(c, launch_zero_outputs(a, c->stream));
         return BRE_OK;
     }
-    // auto (0): kernel 4 on the tile tree.  Hand-over (6): kernel 3 on the small-leaf tree with
-    // kernel 4 on the tile tree taking the packets it hands over (launch_gather's mode 0); with
-    // leaf clusters too large for kernel 3, kernel 4 alone
     int kernel = c->kernel;
-    if (kernel == 5) return gather_chunk(c, a);
-    if (kernel == 0) kernel = 4;
-    else if (kernel == 6) kernel = c->built_leaf2 == 0 ? (c->built_leaf_size <= kProxyMaxLeafHost ? 3 : 4) : 0;
-    if (kernel == 3 && c->built_leaf_size > kProxyMaxLeafHost)
-        return fail(c, BRE_ERR_STATE, "kernel 3 needs BRE_OPT_LEAF_SIZE <= %d", kProxyMaxLeafHost);
-    if (kernel != 2) {
+    if (kernel == 5) {
+        if (seg_index) return fail(c, BRE_ERR_STATE, "kernel 5 gathers in the caller's order only");
+        return gather_chunk(c, a);
+    }
+    if (kernel == 0) kernel = 4;  // the tile kernel on the tile tree built for kernel 0
+    if (kernel == 4) {
         HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
         HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)nseg * (size_t)c->split));
         if (c->roots_split != c->split) {
@@ -404,21 +417,12 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         a.roots = c->roots.as<int32_t>();
         a.partial = c->partial.as<float>();
-        if (kernel == 0) {
-            HIPCHK(c, c->roots2.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
-            if (c->roots2_split != c->split) {
-                HIPCHK(c, launch_roots(c->nodes2.as<Node>(), c->split, c->roots2.as<int32_t>(), c->stream));
-                c->roots2_split = c->split;
-            }
-            a.nodes2 = c->nodes2.as<Node>();
-            a.roots2 = c->roots2.as<int32_t>();
-        }
-        HIPCHK(c, c->redo.ensure((size_t)(nseg + 63) / 64 + 16));
-        a.redo = c->redo.as<uint8_t>();
-        if (c->counters) {
+        if (c->counters || seg_counts) {
             HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
             a.pcnt = c->pcnt.as<int32_t>();
         }
+    } else if (kernel == 2 && seg_index) {
+        return fail(c, BRE_ERR_STATE, "kernel 2 gathers in the caller's order only");
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
@@ -426,31 +430,29 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     return read_counters(c, a.ctr);
 }
 
+// With counters or timing on, copy the counter block back (synchronising) into the stats.
 bre_status read_counters(bre_ctx *c, DevCounters *ctr) {
-    if (c->timing || c->counters) {
-        DevCounters h;
-        HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->timing) {
-            float ms = 0.f;
-            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-            c->stats.gather_ms = ms;
-        }
-        c->stats.candidates = (int64_t)h.candidates;
-        c->stats.contributions = (int64_t)h.contributions;
-        c->stats.node_visits = (int64_t)h.node_visits;
-        c->stats.leaf_visits = (int64_t)h.leaf_visits;
-        c->stats.beam_evals = (int64_t)h.beam_evals;
-        c->stats.ccp_wave_evals = (int64_t)h.ccp_wave_evals;
-        c->stats.prefilter_rejects = (int64_t)h.prefilter_rejects;
-        c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
-        c->stats.max_stack_depth = (int64_t)h.max_stack;
-        c->stats.redo_items = (int64_t)h.redo_items;
-        c->stats.n_chunks = c->n_chunks;
-        if (h.flags & 1u) return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than stack)");
-        if (h.flags & 2u) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix)");
+    if (!(c->timing || c->counters)) return BRE_OK;
+    DevCounters h;
+    HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->timing) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        c->stats.gather_ms = ms;
     }
-    return BRE_OK;
+    c->stats.candidates = (int64_t)h.candidates;
+    c->stats.contributions = (int64_t)h.contributions;
+    c->stats.node_visits = (int64_t)h.node_visits;
+    c->stats.leaf_visits = (int64_t)h.leaf_visits;
+    c->stats.beam_evals = (int64_t)h.beam_evals;
+    c->stats.ccp_wave_evals = (int64_t)h.ccp_wave_evals;
+    c->stats.prefilter_rejects = (int64_t)h.prefilter_rejects;
+    c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
+    c->stats.max_stack_depth = (int64_t)h.max_stack;
+    c->stats.redo_items = 0;
+    c->stats.n_chunks = c->n_chunks;
+    return check_flags(c);
 }
 
 // exclusive scan of the camera slots' valid flags into cam_offs
@@ -496,16 +498,17 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->redo,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
-                     &c->seg_depth, &c->grid_dens, &c->nodes2, &c->roots2, &c->ch_bounds, &c->ch_counts,
+                     &c->seg_depth, &c->ch_bounds, &c->ch_counts,
                      &c->ch_offsets, &c->ch_range, &c->ch_scan_tmp, &c->ch_box, &c->ch_cent, &c->ch_slo, &c->ch_shi,
                      &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
                      &c->ss_t, &c->ss_pix};
     for (DevMem *m : all) m->release();
+    if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -520,7 +523,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_COUNTERS: c->counters = value != 0; return BRE_OK;
     case BRE_OPT_TIMING: c->timing = value != 0; return BRE_OK;
     case BRE_OPT_KERNEL:
-        if (value < 0 || value > 6) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0..6");
+        if (value != 0 && value != 2 && value != 4 && value != 5)
+            return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_KERNEL must be 0, 2, 4 or 5 (kernels 1, 3 and 6 were removed)");
         c->kernel = (int)value;
         return BRE_OK;
     case BRE_OPT_LEAF_SIZE:
@@ -561,12 +565,16 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->shard_count = (int)value;
         if (c->shard_rank >= c->shard_count) c->shard_rank = 0;
         return BRE_OK;
-    case 100: c->debug_mode = (int)value; return BRE_OK;  // internal: timing-only ablations
-    case 101: c->stack_limit = (int)value; return BRE_OK;  // internal: shrink kernel 3's stack (tests)
-    case 102: c->occupancy = (int)value; return BRE_OK;    // internal: kernel 4 register budget (1 or 8)
-    case 104: c->tile_mode = (int)value; return BRE_OK;    // internal: kernel 4 leaf order (tests, sweeps)
-    case 105: c->sort_key = (int)value; return BRE_OK;     // internal: segment sort key (sweeps)
-    case 103: c->loose_cos = (float)value * 1e-4f; return BRE_OK;  // internal: kernel 3 coherence cut (1e-4)
+    case 101:  // internal: traversal stack entries to use, 0 = all (tests force an overflow)
+        if (value < 0 || value > kStackDepth) return fail(c, BRE_ERR_INVALID_ARG, "stack cap must be in 0..%d", kStackDepth);
+        c->stack_cap = (int)value;
+        return BRE_OK;
+    case 102:  // internal: tile kernel register budget, min waves per SIMD (sweeps)
+        if (value != 1 && value != 6 && value != 7 && value != 8)
+            return fail(c, BRE_ERR_INVALID_ARG, "occupancy must be 1, 6, 7 or 8");
+        c->occupancy = (int)value;
+        return BRE_OK;
+    case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
 }
@@ -590,8 +598,7 @@ bre_status bre_set_stream(bre_ctx *c, void *stream) {
 
 bre_status bre_synchronize(bre_ctx *c) {
     if (!c) return BRE_ERR_INVALID_ARG;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BRE_OK;
+    return check_flags(c);
 }
 
 bre_status bre_get_stats(const bre_ctx *c, bre_stats *out) {
@@ -730,7 +737,8 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     st = build(c, total, c->in_start.as<float>(), c->in_end.as<float>(), c->in_radius.as<float>(),
                c->in_power.as<float>());
     if (st != BRE_OK) return st;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    st = check_flags(c);  // also reports an earlier asynchronous gather's device errors
+    if (st != BRE_OK) return st;
     c->beams_kept = true;
     c->stats.n_photons = n_photons;
     c->stats.photon_ms = photon_ms;
@@ -755,8 +763,7 @@ bre_status bre_get_beams(bre_ctx *c, int64_t capacity, float *start, float *end,
     HIPCHK(c, hipMemcpyAsync(end, c->in_end.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(radius, c->in_radius.ptr, K * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(power, c->in_power.ptr, K * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BRE_OK;
+    return check_flags(c);
 }
 
 static bre_status check_scene(bre_ctx *c, const bre_scene *scene, const char *fn) {
@@ -846,7 +853,8 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
         HIPCHK(c, hipEventSynchronize(c->ev[1]));
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    st = check_flags(c);
+    if (st != BRE_OK) return st;
     c->cam_nseg = n;
     c->cam_npix = (int64_t)width * height;
     c->stats.n_camera_segments = n;
@@ -855,17 +863,19 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     return BRE_OK;
 }
 
-bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
-    if (!c) return BRE_ERR_INVALID_ARG;
+// The camera segments of the last camera pass against the beam set, in the production order: the
+// segments only add into their pixels, so the packet kernel takes them in a coherence order
+// (bre_sort.hip); per-segment outputs (optional) are scattered back to the camera-pass order.
+static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_seg_rgb, int32_t *d_seg_counts) {
     if (c->cam_npix == 0) return fail(c, BRE_ERR_STATE, "bre_gather_camera: no camera pass yet");
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     const int64_t n = c->cam_nseg;
-    if (!c->sort_segments || n < 2)
+    const bool sortable = c->kernel == 0 || c->kernel == 4;  // kernels 2 / 5 write in the caller's order
+    if (!c->sort_segments || n < 2 || (!sortable && (d_seg_rgb || d_seg_counts)))
         return gather_device(c, n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
-                             c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, nullptr, nullptr);
-    // the segments only add into their pixels here, so the packet kernels may take them in a
-    // coherence order (bre_sort.hip)
+                             c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
+                             d_seg_counts);
     const size_t N = (size_t)n;
     HIPCHK(c, c->ss_bounds.ensure(8 * sizeof(unsigned int)));
     HIPCHK(c, c->ss_keys.ensure(N * sizeof(unsigned long long)));
@@ -885,7 +895,19 @@ bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
                c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
                c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
-    return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, nullptr, nullptr);
+    // ss_vals_alt[i] = the camera-pass index of sorted segment i (the sort's permutation)
+    return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, d_seg_rgb, d_seg_counts,
+                         (d_seg_rgb || d_seg_counts) ? c->ss_vals_alt.as<int32_t>() : nullptr);
+}
+
+bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    return gather_camera(c, R, d_accum, nullptr, nullptr);
+}
+
+bre_status bre_gather_camera_segments(bre_ctx *c, float R, float *d_accum, float *d_seg_rgb, int32_t *d_seg_counts) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    return gather_camera(c, R, d_accum, d_seg_rgb, d_seg_counts);
 }
 
 bre_status bre_get_segments(bre_ctx *c, int64_t capacity, float *o, float *p, float *d, float *tmax, int32_t *pixel,
@@ -906,13 +928,12 @@ bre_status bre_get_segments(bre_ctx *c, int64_t capacity, float *o, float *p, fl
     HIPCHK(c, hipMemcpyAsync(tmax, c->seg_t.ptr, K * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(pixel, c->seg_pix.ptr, K * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(depth, c->seg_depth.ptr, K * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BRE_OK;
+    return check_flags(c);
 }
 
 static bre_status check_params(bre_ctx *c, const bre_render_params *rp) {
     if (!rp) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null params");
-    if (rp->width < 1 || rp->height < 1 || rp->photons_per_iteration < 0 || rp->start_iteration < 0 ||
+    if (rp->width < 1 || rp->height < 1 || rp->start_iteration < 0 ||
         rp->end_iteration < rp->start_iteration || rp->max_depth < 1 || rp->max_depth > BRE_MAX_DEPTH)
         return fail(c, BRE_ERR_INVALID_ARG, "bre_render: bad parameters");
     return BRE_OK;
@@ -925,7 +946,10 @@ bre_status bre_render_iteration(bre_ctx *c, const bre_scene *scene, const bre_re
     if (st != BRE_OK) return st;
     if (!d_ld) return fail(c, BRE_ERR_INVALID_ARG, "bre_render_iteration: null Ld buffer");
     const float R = bre_beam_radius_at(rp->initial_radius, rp->alpha, iteration);
-    st = bre_trace_photons(c, scene, rp->photons_per_iteration, iteration, rp->max_depth, R, nullptr);
+    // photonsperiteration <= 0 means the film's pixel count (photonbeam.h:37-39, the -1 default)
+    const int64_t photons =
+        rp->photons_per_iteration > 0 ? rp->photons_per_iteration : (int64_t)rp->width * rp->height;
+    st = bre_trace_photons(c, scene, photons, iteration, rp->max_depth, R, nullptr);
     if (st != BRE_OK) return st;
     st = bre_camera_pass(c, scene, rp->width, rp->height, iteration, rp->max_depth, rp->render_surfaces,
                          rp->render_media, d_ld, nullptr);
@@ -951,8 +975,12 @@ bre_status bre_render_progressive(bre_ctx *c, const bre_scene *scene, const bre_
     for (int it = rp->start_iteration; st == BRE_OK && it < rp->end_iteration; ++it) {
         st = bre_render_iteration(c, scene, rp, it, ld);
         if (st != BRE_OK) break;
-        // photonbeam.cpp:564: write at the last iteration and every write_frequency iterations
-        const bool write = (it + 1 == rp->end_iteration) || (write_frequency > 0 && (it + 1) % write_frequency == 0);
+        // photonbeam.cpp:564: write at the last iteration and whenever (iter + 1) % writeFrequency == 0,
+        // negative frequencies included (-k fires every k iterations); the reference's default
+        // 1 << 31 wraps to INT32_MIN and never fires, and 0 (a division by zero there) means never
+        const bool periodic = write_frequency != 0 && write_frequency != INT32_MIN &&
+                              (it + 1) % write_frequency == 0;
+        const bool write = (it + 1 == rp->end_iteration) || periodic;
         if (!write || !on_image) continue;
         h.resize((size_t)npix * 3);
         img.resize(h.size());
@@ -965,7 +993,8 @@ bre_status bre_render_progressive(bre_ctx *c, const bre_scene *scene, const bre_
         if (st == BRE_OK && on_image(it, img.data(), user) != 0)
             st = fail(c, BRE_ERR_STATE, "bre_render: image callback stopped the render after iteration %d", it);
     }
-    (void)hipStreamSynchronize(c->stream);
+    const bre_status fst = check_flags(c);  // the last iteration's gather
+    if (st == BRE_OK) st = fst;
     (void)hipFree(ld);
     return st;
 }
@@ -1150,8 +1179,7 @@ bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, 
     if (daccum) HIPCHK(c, hipMemcpyAsync(accum, daccum, P * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (dseg) HIPCHK(c, hipMemcpyAsync(seg_rgb, dseg, S * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (dcnt) HIPCHK(c, hipMemcpyAsync(seg_counts, dcnt, S * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return BRE_OK;
+    return check_flags(c);
 }
 
 float bre_beam_radius_at(float initial_radius, float alpha, int iteration) {

@@ -393,7 +393,14 @@ hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
 hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (nvalid == 0) return hipSuccess;
     const int K = b.leaf_size;
-    const int nleaf = (int)((nvalid + K - 1) / K);
+    if (K < 1) return hipErrorInvalidValue;
+    const int64_t nleaf64 = (nvalid + K - 1) / K;
+    // the hierarchy writes nleaf - 1 nodes (1 for a single leaf), nleaf leaf parents and nleaf - 1
+    // refit counters: refuse buffers sized for another leaf size instead of writing past them
+    if (nleaf64 > INT32_MAX || (uint64_t)(nleaf64 > 1 ? nleaf64 - 1 : 1) > b.nodes_cap ||
+        (nleaf64 > 1 && ((uint64_t)nleaf64 > b.leaf_parent_cap || (uint64_t)(nleaf64 - 1) > b.visit_cap)))
+        return hipErrorInvalidValue;
+    const int nleaf = (int)nleaf64;
     if (nleaf == 1) {
         hipLaunchKernelGGL(k_single, dim3(1), dim3(64), 0, s, b.recs, nvalid, K, b.nodes);
         return hipGetLastError();

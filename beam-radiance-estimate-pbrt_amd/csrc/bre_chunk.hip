@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kChunkBlock) void k_gather_chunk(
                 if (h0 && h1) {
                     const bool first0 = !(te1 < te0);
                     if (sp >= kChunkStack) {
-                        atomicOr(&ctr->flags, 1u);
+                        atomicOr(&ctr->flags, kFlagStack);
                         break;
                     }
                     stk[sp][tid] = first0 ? c1 : c0;
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(kChunkBlock) void k_gather_chunk(
         if (accum) {
             const int32_t px = pixel[s];
             if (px < 0 || px >= npix) {
-                atomicOr(&ctr->flags, 2u);
+                atomicOr(&ctr->flags, kFlagPixel);
             } else if (acc.r != 0.f || acc.g != 0.f || acc.b != 0.f) {
                 atomicAdd(&accum[3 * (int64_t)px], acc.r);
                 atomicAdd(&accum[3 * (int64_t)px + 1], acc.g);

@@ -35,21 +35,26 @@ constexpr int32_t kEmptyChild = INT32_MIN;
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
 constexpr int kMaxSplit = 64;          // max work roots (subtrees) per gather
-constexpr int kProxyMaxLeafHost = 4;   // kernel 3 candidate list sized for leaf clusters <= 4
 
-// Error / counter block in device memory (zeroed per call).
+// DevCounters::flags bits.  The host reads the word at every synchronising call and turns a set bit
+// into an error (bre_api.hip: check_flags), whatever the counters option.
+constexpr unsigned int kFlagStack = 1u;  // a traversal stack overflowed: contributions were dropped
+constexpr unsigned int kFlagPixel = 2u;  // a seg_pixel index outside [0, npix): the segment was skipped
+
+// Error / counter block in device memory (the counters are zeroed per gather; `flags` is sticky
+// until the host has read it).
 struct DevCounters {
     unsigned long long candidates;
     unsigned long long contributions;
     unsigned long long node_visits;
-    unsigned long long leaf_visits;     // kernel 1: leaf clusters evaluated (per wave)
-    unsigned long long beam_evals;      // kernel 1: beam records evaluated (per wave)
-    unsigned long long ccp_wave_evals;  // kernel 1: exact closest-point executions (per wave)
-    unsigned long long prefilter_rejects;  // kernel 1: lane-level rejects by the line-distance filter
-    unsigned long long useful_beam_evals;  // kernel 1: beam evaluations with >= 1 lane passing the box
-    unsigned long long redo_items;         // kernel 3: (packet, subtree) items handed to kernel 1
-    unsigned int flags;  // bit0 stack overflow, bit1 pixel index out of range, bit2 proxy-stack overflow
-    unsigned int max_stack;  // kernel 3: deepest LDS node stack seen
+    unsigned long long leaf_visits;        // leaf tiles visited (per wave)
+    unsigned long long beam_evals;         // beam records staged (per wave)
+    unsigned long long ccp_wave_evals;     // exact-stage batches of <= 64 pairs (per wave)
+    unsigned long long prefilter_rejects;  // lane-level candidate rejects by the line-distance prefilters
+    unsigned long long useful_beam_evals;  // beams kept by the packet bundle test
+    unsigned long long redo_items;         // unused (kept for the stats layout)
+    unsigned int max_stack;
+    unsigned int flags;  // kFlag* bits (sticky)
 };
 
 struct BuildBuffers {
@@ -73,6 +78,8 @@ struct BuildBuffers {
     BeamRec *recs;      // nvalid
     float4 *pow;        // nvalid, powerEnd * 1e-5f
     Node *nodes;        // max(nleaf-1, 1)
+    // capacities (elements) of the hierarchy's output / scratch buffers, checked by launch_hierarchy
+    uint64_t nodes_cap = 0, leaf_parent_cap = 0, visit_cap = 0;
 };
 
 // One capsule chunk of a beam LINE (kernel 5, bre_chunk.hip): 64 B, same leading lo/hi as
@@ -102,32 +109,24 @@ struct GatherArgs {
     const int32_t *pixel;
     float R;
     int64_t npix;
-    float *accum;      // may be null
-    float *seg_rgb;    // may be null
-    int32_t *seg_counts;  // may be null
+    float *accum;          // may be null
+    float *seg_rgb;        // may be null
+    int32_t *seg_counts;   // may be null
+    const int32_t *seg_index;  // may be null: seg_rgb / seg_counts entry of gathered segment s is seg_index[s]
     const BeamRec *recs;
     const float4 *pow;
     const Node *nodes;
     int64_t nvalid;
     int leaf_size;
     DevCounters *ctr;
-    // wave kernel: subtree split
+    // tile kernel: subtree split
     const int32_t *roots;  // [split] work roots + [split] = count
     int split;             // S, power of two <= kMaxSplit
     float *partial;        // [split][nseg][3]
-    int32_t *pcnt;         // [split][nseg][2] per-subtree counts (counters only)
+    int32_t *pcnt;         // [split][nseg][2] per-subtree counts (counters / contribution counting)
     bool prefilter;
-    int debug_mode;        // 0 normal; 1 timing-only: traversal without leaf evaluation
-    int stack_limit;       // kernel 3 LDS stack entries to use (0 = all); tests force the fallback
-    int occupancy;         // kernel 3 register budget: min waves per SIMD (1, 6 or 8)
-    uint8_t *redo;         // kernel 3: [packets] flags of packets handed to kernel 1 (or 4)
-    // auto mode (kernel 0): the tile tree over the same beam records for kernel 4's hand-over
-    const Node *nodes2;
-    const int32_t *roots2;
-    int leaf2;
-    float loose_cos;       // kernel 3: packets whose lanes' directions spread wider than this cosine
-                           // are handed over (0: default)
-    int tile_mode;         // kernel 4 leaf order: 0 box test first, 1 line-distance prefilter first
+    int occupancy;         // tile kernel register budget: min waves per SIMD (1, 6, 7 or 8)
+    int stack_cap;         // traversal stack entries to use (0 = all); tests force an overflow
 };
 
 // capsule-chunk index (bre_chunk.hip)

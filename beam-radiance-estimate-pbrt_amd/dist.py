@@ -1,12 +1,15 @@
 """Multi-GPU decomposition of the gather: image tiles across ranks, beams replicated.
 
 The reference's camera pass already works in 16x16 pixel tiles (photonbeam.cpp:345-347, 444-557);
-here those tiles are dealt round-robin to the ranks (one process per GPU), every rank holds the
-whole beam set (regenerated from the same seeds, or broadcast once per pass) and builds its own
-BVH, and each pixel is written by exactly one rank.  The only exchange is one framebuffer
-reduction per written image (photonbeam.cpp:565-584), an RCCL reduce over xGMI with the "nccl"
-backend (gloo in the CPU tests).  Because ownership is disjoint, the reduced image is bit-identical
-to a single-rank render: every pixel is x + 0 + ... + 0.
+here those tiles are dealt round-robin to the ranks (one process per GPU; libbre's camera pass walks
+only the rank's tiles, BRE_OPT_SHARD_RANK / BRE_OPT_SHARD_COUNT).  Every rank holds the whole beam
+set (each traces the same photons from the same per-photon PCG32 sequences, photonbeam.cpp:386-389,
+so the data path has no communication) and builds its own BVH; each pixel is written by exactly
+one rank.  The only exchange is one framebuffer GATHER per written image (photonbeam.cpp:565-584):
+every rank packs the pixels of its own tiles into a contiguous band (1/N of the film) and the bands
+are gathered to the root over RCCL (backend "nccl") or gloo (CPU tests), which scatters them back
+into the full film.  Ownership is disjoint, so the gathered film equals the sum of the ranks'
+partial films exactly.
 """
 from __future__ import annotations
 
@@ -27,27 +30,48 @@ def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16) -> np.nda
 
 
 class ShardedFrame:
-    """Full-resolution RGB accumulation buffer of one rank (zeros outside its tiles)."""
+    """Full-resolution RGB accumulation buffer of one rank (only its own tiles are ever written)."""
 
     def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16):
         import torch
 
-        self.w, self.h, self.rank, self.world = w, h, rank, world
+        self.w, self.h, self.rank, self.world, self.tile = w, h, rank, world, tile
         self.pixels = tile_pixels(w, h, rank, world, tile)
         self.accum = torch.zeros((w * h, 3), dtype=torch.float32, device=device)
+        self.device = device
+        self._band = None
+        if world > 1:
+            counts = [tile_pixels(w, h, r, world, tile).shape[0] for r in range(world)]
+            self.band_len = max(counts)
+            self._idx = torch.from_numpy(self.pixels).to(device)
+            self._all_idx = [torch.from_numpy(tile_pixels(w, h, r, world, tile)).to(device) for r in range(world)]
 
     @property
     def npix(self) -> int:
         return self.w * self.h
 
-    def reduce_to_root(self, root: int = 0):
-        """One collective per written image: sum the disjoint partial frames onto `root`."""
+    def gather_to_root(self, root: int = 0):
+        """One collective per written image: each rank's band of owned pixels (packed, 1/N of the
+        film) is gathered to `root`, which scatters the bands into the full film.  Returns the full
+        film on the root (the rank's own partial film elsewhere)."""
+        import torch
         import torch.distributed as dist
 
-        if self.world > 1:
-            dist.reduce(self.accum, dst=root)
+        if self.world == 1:
+            return self.accum
+        band = torch.zeros((self.band_len, 3), dtype=torch.float32, device=self.device)
+        band[: self._idx.shape[0]] = self.accum.index_select(0, self._idx)
+        parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(band, gather_list=parts, dst=root)
+        if self.rank == root:
+            for r, idx in enumerate(self._all_idx):
+                if r != root:
+                    self.accum.index_copy_(0, idx, parts[r][: idx.shape[0]])
         return self.accum
 
+    # the round-1 name (a reduce of full frames); kept as an alias of the gather
+    reduce_to_root = gather_to_root
+
     def image(self, iteration: int):
-        """L = Ld / (iter + 1)  (photonbeam.cpp:578), on the root after reduce_to_root()."""
+        """L = Ld / (iter + 1)  (photonbeam.cpp:578), on the root after gather_to_root()."""
         return self.accum / float(iteration + 1)

@@ -74,7 +74,7 @@ bre_status bre_pbrt_get_render_params(const bre_pbrt *p, int32_t quick, bre_rend
     out->render_media = pp.renderMedia;
     out->initial_radius = pp.initialBeamRadius;
     out->alpha = pp.alpha;
-    if (write_frequency) *write_frequency = pp.writeFrequency > 0 ? pp.writeFrequency : 0;
+    if (write_frequency) *write_frequency = pp.writeFrequency;  // bre_render_progressive applies the reference's modulo
     return BRE_OK;
 }
 

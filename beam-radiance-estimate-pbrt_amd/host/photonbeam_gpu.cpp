@@ -148,7 +148,7 @@ bool PhotonBeamIntegrator::Render(const bre_scene &scene) {
     rp.alpha = params_.alpha;
     written_ = 0;
     // the reference's default 1 << 31 is INT_MIN, which never divides iter + 1: "at the end only"
-    const int32_t wf = params_.writeFrequency > 0 ? params_.writeFrequency : 0;
+    const int32_t wf = params_.writeFrequency;  // the reference's (iter + 1) % writeFrequency, negatives included
     const bre_status st = bre_render_progressive(ctx_, &scene, &rp, wf, &PhotonBeamIntegrator::OnImage, this);
     if (st != BRE_OK) {
         if (err_.empty()) err_ = bre_last_error(ctx_);

@@ -11,20 +11,24 @@ camera segment (photonbeam.cpp:494-508).  value = segments gathered by all ranks
 time of the timed steps.  Iteration k of the timed loop is the reference's iteration k (radius
 schedule and sampler indices included), so `--steps 16` is exactly the C2 render.
 
-`--workload synthetic` = SURVEY.md §8d synthetic-fog kernel-only set (1M beams, seed 12345; one
-camera segment per pixel, seed 777): a step is BVH build + gather.
+Multi-GPU (`--gpus N`): one process per GPU.  Launched by torch.distributed.run (WORLD_SIZE set) it
+joins that group; launched alone with N > 1 it starts N rank processes itself (a torch.distributed.run
+child, before any GPU call) and exits with its status.  Default scaling is STRONG: one film (the
+workload's W x H) whose 16x16 tiles (photonbeam.cpp:345-347) are dealt round-robin to the ranks; every
+rank traces the same photons (per-photon PCG32 sequences, no communication) and builds its own BVH;
+the ranks' bands of owned pixels are gathered to rank 0 once per written image (the last step), one
+RCCL gather.  `--scaling weak` gives every rank its own film of the same size (N independent renders).
 
-Multi-GPU (weak scaling): the film is 512 x (512*N); its 16x16 tiles (photonbeam.cpp:345-347) are
-dealt round-robin to the N ranks; every rank traces the same photons (per-photon PCG32 sequences,
-so no communication) and builds its own BVH; the framebuffer partial sums are reduced to rank 0
-once per written image (the last step), one RCCL reduce.
-
-Also reported: `roofline` (SURVEY.md §8d algorithmic bytes of the gather kernel vs HBM peak; the
-gather kernel's average duration measured with HIP events on the stream it is launched on;
-`traffic` = PMC FETCH_SIZE+WRITE_SIZE per launch from the committed rocprofv3 summary of the same
-workload, when present) and `cpu_baseline` (the oracle's CPU restatement of the reference
-algorithm — SAH tree, per-query vector<shared_ptr>, all host threads — timed on a bounded sample
-of the same segments and beams; rank 0, N=1).
+Also reported (rank 0, N = 1):
+* `roofline` — HBM: the tile kernel's algorithmic bytes per launch (what its packets must read: node
+  and beam lines of the visited tiles, the segments, the partial sums; counted live by the counter
+  pass) / its HIP-event launch time; `traffic` = HBM bytes per launch from this run's own rocprofv3
+  PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); `issue` = SQ counters of the same
+  passes (VALU issue and LDS utilisation: the kernel's real bound); the SURVEY §8d reference-tree
+  byte model is kept as `ref_model_*` (not a fraction: one staged beam line feeds 64 lanes).
+* `cpu_baseline` — the oracle's CPU restatement of the reference algorithm (SAH tree, per-query
+  vector<shared_ptr>, all host threads, plus 1 thread), timed on bounded samples of the same
+  segments and beams at the first and last timed iterations.
 """
 from __future__ import annotations
 
@@ -32,7 +36,10 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -41,120 +48,126 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
+CUS, SIMDS = 256, 4     # VALU issue peak: one wave64 instruction per 2 clocks per SIMD-32
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None,
                     help="timed iterations (default: c2 16 = the whole 16-spp render, c5 10 passes, else 4)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "synthetic"], default="c2",
-                    help="BASELINE.json configs[1..4] (SURVEY.md §8d) or the kernel-only synthetic set")
-    ap.add_argument("--photons", type=int, default=None, help="photons per iteration (c2 1M, c3 5M, c4 20M, c5 50M)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="BASELINE.json configs[1..4] (SURVEY.md §8d), c4-1m (the 2K tiled film at C2's 1M "
+                         "photons), or the kernel-only synthetic set")
+    ap.add_argument("--photons", type=int, default=None, help="photons per iteration")
     ap.add_argument("--beams", type=int, default=1_000_000, help="synthetic: beams")
-    ap.add_argument("--width", type=int, default=None, help="film width (c2 512, c3/c5 1024, c4 2048)")
-    ap.add_argument("--height", type=int, default=None, help="film height per GPU (weak) or total (strong)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
-                    help="weak: a W x (H*N) film, H rows per GPU (default); strong: one W x H film split by "
-                         "16x16 tiles over the N GPUs (c4 default)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong (default): one film split by 16x16 tiles over the N GPUs; weak: a film per GPU")
     ap.add_argument("--grid-n", type=int, default=64, help="c3/c5: smoke density grid resolution")
-    ap.add_argument("--radius", type=float, default=0.01, help="initialbeamradius (c2) / R (synthetic)")
+    ap.add_argument("--radius", type=float, default=0.01, help="initialbeamradius (scenes) / R (synthetic)")
     ap.add_argument("--alpha", type=float, default=0.5)
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=1)
-    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet (kernels 1/3)")
+    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet")
     ap.add_argument("--prefilter", type=int, default=1)
     ap.add_argument("--chunk-len", type=int, default=400, help="kernel 5: chunk length in units of E/100")
     ap.add_argument("--chunk-leaf", type=int, default=1, help="kernel 5: chunks per LBVH leaf")
     ap.add_argument("--sort-segments", type=int, default=1, help="coherence-sort the camera segments (0/1)")
-    ap.add_argument("--debug-mode", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--loose-cos", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--tile-mode", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes of the roofline")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
                     help="synthetic: camera primary segments or incoherent bounce segments")
-    ap.add_argument("--profile-summary", default=None,
-                    help="rocprofv3 PMC summary (profiles/*/profile_summary.json) for roofline.traffic")
     ap.add_argument("--json-out", default=None)
-    a = ap.parse_args()
-    preset = WORKLOADS.get(a.workload, WORKLOADS["c2"])
-    for k in ("steps", "photons", "width", "height", "scaling"):
+    a = ap.parse_args(argv)
+    preset = WORKLOADS[a.workload]
+    for k in ("steps", "photons", "width", "height"):
         if getattr(a, k) is None:
             setattr(a, k, preset[k])
     return a
 
 
-# BASELINE.json configs[1..4].  c4/c5 are 8-GPU configurations: at N=1 they run
-# as stated (long) unless --photons / --width / --height scale them down.
+# BASELINE.json configs[1..4].  c4/c5 are 8-GPU configurations: at N=1 they run as
+# stated (long) unless --photons / --width / --height scale them down.  c4-1m is the 2K tiled film
+# at C2's photon count (the scaling study that fits one GPU's time budget).
 WORKLOADS = {
-    "c2": dict(steps=16, photons=1_000_000, width=512, height=512, scaling="weak", medium="fog", g=0.0),
-    "c3": dict(steps=4, photons=5_000_000, width=1024, height=1024, scaling="weak", medium="smoke", g=0.7),
-    "c4": dict(steps=4, photons=20_000_000, width=2048, height=2048, scaling="strong", medium="fog", g=0.0),
-    "c5": dict(steps=10, photons=50_000_000, width=1024, height=1024, scaling="strong", medium="smoke", g=0.7),
-    "synthetic": dict(steps=10, photons=0, width=512, height=512, scaling="weak", medium="fog", g=0.0),
+    "c2": dict(steps=16, photons=1_000_000, width=512, height=512, medium="fog", g=0.0),
+    "c3": dict(steps=4, photons=5_000_000, width=1024, height=1024, medium="smoke", g=0.7),
+    "c4": dict(steps=4, photons=20_000_000, width=2048, height=2048, medium="fog", g=0.0),
+    "c4-1m": dict(steps=4, photons=1_000_000, width=2048, height=2048, medium="fog", g=0.0),
+    "c5": dict(steps=10, photons=50_000_000, width=1024, height=1024, medium="smoke", g=0.7),
+    "synthetic": dict(steps=10, photons=0, width=512, height=512, medium="fog", g=0.0),
 }
 
-
-# V (reference-tree node tests) and C (candidates) per estimate of each workload's iteration 0,
-# measured by the oracle at N=1 (bench.py's CPU leg, profiles/r09/bench.json); used for the
-# roofline fields when this run has no CPU leg.  The beams and segments do not depend on N.
-ROOFLINE_REF = {
-    "c2": {"V_ref_tree": 1365412.6795491143, "C": 420520.3309178744,
-           "source": "profiles/r09/bench.json (oracle SAH tree, CPU sample of iteration 0)"},
-}
+KERNEL_NAMES = {0: "kernel 0: wave packets over 64-beam leaf tiles, packet bundle reject, separable per-lane "
+                   "prefilter, wavefront-compacted exact stage",
+                2: "kernel 2: thread-per-segment", 4: "kernel 4: tile kernel on BRE_OPT_LEAF_SIZE leaves",
+                5: "kernel 5: capsule-chunk index"}
 
 
-KERNEL_NAMES = {0: "auto (kernel 4: leaf tiles of 64 beams, packet bundle reject, compacted pair queue)", 1: "depth-first wave-packet",
-                2: "thread-per-segment", 3: "packet-proxy + depth-first hand-over",
-                4: "leaf tiles + wavefront-compacted pair queue",
-                5: "capsule-chunk index (contributing pairs only)",
-                6: "hand-over (packet-proxy kernel 3 + leaf-tile kernel 4)"}
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a process group: start N ranks (torch.distributed.run, one per GPU) as a
+    child process — nothing here has touched the GPU — and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
     bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
     dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if env_world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world, rank = dist.get_world_size(), dist.get_rank()  # n_gpus from the live process group
     else:
         torch.cuda.set_device(0)
+        world, rank = 1, 0
+    if args.gpus != world and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but the process group has {world} ranks; reporting {world}",
+              file=sys.stderr)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    W, H = args.width, args.height * (world if args.scaling == "weak" else 1)
-    frame = dmod.ShardedFrame(W, H, rank, world, device=dev)
+    strong = args.scaling == "strong"
+    frame = dmod.ShardedFrame(args.width, args.height, rank if strong else 0, world if strong else 1, device=dev)
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
     g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
     if args.kernel == 5:
         g.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
         g.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
-    if args.debug_mode:
-        g.set_option(100, args.debug_mode)
     if args.occupancy:
         g.set_option(102, args.occupancy)
-    if args.loose_cos:
-        g.set_option(103, args.loose_cos)
     if args.tile_leaf:
         g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
-    if args.tile_mode >= 0:
-        g.set_option(104, args.tile_mode)
     if args.sort_key >= 0:
         g.set_option(105, args.sort_key)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
@@ -164,9 +177,15 @@ def main():
     g.set_stream(stream.cuda_stream)
 
     if args.workload != "synthetic":
-        wl = SceneWorkload(args, bre, g, frame, rank, world)
+        wl = SceneWorkload(args, bre, g, frame, rank if strong else 0, world if strong else 1)
     else:
-        wl = SyntheticWorkload(args, bre, g, frame, rank, world, dev)
+        wl = SyntheticWorkload(args, bre, g, frame, dev)
+
+    if args.pmc_child:  # one untimed iteration for the parent's rocprofv3 PMC pass
+        wl.step(0, None, scratch=True)
+        g.synchronize()
+        g.close()
+        return
 
     for k in range(args.warmup):
         wl.step(k, None, scratch=True)
@@ -180,14 +199,15 @@ def main():
     nseg_local = 0
     for k in range(args.steps):
         nseg_local += wl.step(k, events[k], scratch=False)
-        if k == args.steps - 1:
-            frame.reduce_to_root(0)  # one RCCL reduce per written image (no-op at N=1)
+        if k == args.steps - 1 and strong:
+            frame.gather_to_root(0)  # one RCCL gather per written image (no-op at N=1)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    gather_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    gather_per_step = [a.elapsed_time(b) for a, b in events]
+    gather_ms = float(np.mean(gather_per_step))
     if world > 1:
         tt = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -200,19 +220,17 @@ def main():
     value = total_seg / elapsed
 
     # untimed: one more step with counters and per-phase HIP-event timing inside libbre
+    diag, st = {}, None
     if not args.no_diag:
         g.set_option(bre.OPT_COUNTERS, 1)
         g.set_option(bre.OPT_TIMING, 1)
         diag = wl.diagnostics()
-    else:
-        diag = {}
-    st = g.stats()
-    nseg_d = max(st["n_segments"], 1)
-    waves = (nseg_d + 63) // 64
-    c_mean = st["candidates"] / nseg_d
+        st = g.stats()
+        g.set_option(bre.OPT_COUNTERS, 0)
+        g.set_option(bre.OPT_TIMING, 0)
 
     result = {
-        "metric": ("beam-radiance estimates/sec at 1M photons" if args.workload in ("c2", "synthetic") else
+        "metric": ("beam-radiance estimates/sec at 1M photons" if args.photons in (0, 1_000_000) else
                    f"beam-radiance estimates/sec at {args.photons / 1e6:g}M photons"),
         "value": value,
         "unit": "estimates/s",
@@ -225,61 +243,37 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": wl.data,
-        "config": wl.config(),
+        "config": wl.config(world),
         "estimates_per_step_per_gpu": nseg_local / args.steps,
         "gather_kernel_ms": gather_ms,
-        "candidates_per_estimate": c_mean,
-        "contributions_per_estimate": st["contributions"] / nseg_d,
-        "candidate_pair_tests_per_s": c_mean * value,
-        "node_visits_per_wave": st["node_visits"] / waves,
-        "leaf_visits_per_wave": st["leaf_visits"] / waves,
-        "beam_evals_per_wave": st["beam_evals"] / waves,
-        "ccp_wave_evals_per_wave": st["ccp_wave_evals"] / waves,
-        "max_stack_depth": st["max_stack_depth"],
-        "redo_items": st["redo_items"],
-        "prefilter_rejects_per_estimate": st["prefilter_rejects"] / nseg_d,
-        "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
-        "chunks": st.get("n_chunks", 0),
+        "gather_ms_per_step": gather_per_step if rank == 0 else None,
     }
+    if st is not None:
+        nseg_d = max(st["n_segments"], 1)
+        items = (nseg_d + 63) // 64 * args.split  # (packet, subtree) work items = waves
+        result.update({
+            "candidates_per_estimate": st["candidates"] / nseg_d,
+            "contributions_per_estimate": st["contributions"] / nseg_d,
+            "candidate_pair_tests_per_s": st["candidates"] / nseg_d * value,
+            "node_visits_per_wave": st["node_visits"] / items,
+            "leaf_visits_per_wave": st["leaf_visits"] / items,
+            "beam_lines_staged_per_wave": st["beam_evals"] / items,
+            "exact_batches_per_wave": st["ccp_wave_evals"] / items,
+            "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
+        })
     result.update(diag)
 
-    def roofline(v_ref, c_ref, source):
-        # SURVEY.md §8d algorithmic bytes per estimate: 32 + 12 + 32*V + 40*C, V and C from the
-        # reference SAH tree (oracle) on a CPU sample of the same workload
-        bytes_per_est = 32 + 12 + 32 * v_ref + 40 * c_ref
-        per_launch = bytes_per_est * wl.segments_per_gather()
-        achieved = per_launch / (gather_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.profile_summary or wl.default_profile())
-        return {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": traffic,
-            # the PMC-measured bytes per launch over this run's launch time: the HBM/fabric
-            # bandwidth the kernel actually draws (the profile's launches average the same command)
-            "traffic_GBps": traffic / (gather_ms * 1e-3) / 1e9 if traffic else None,
-            "traffic_frac": traffic / (gather_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if traffic else None,
-            "algorithmic_bytes_per_launch": per_launch,
-            "bytes_per_estimate": bytes_per_est,
-            "V_ref_tree": v_ref,
-            "C": c_ref,
-            "V_C_source": source,
-            "kernel": "gather (k_gather_tile; k_gather_proxy too in hand-over mode)",
-        }
-
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(wl.cpu_beams(), wl.cpu_segments(), wl.cpu_radius(), args.cpu_seconds, wl.name)
+        cpu = cpu_baseline(wl, args, gather_per_step)
         result["cpu_baseline"] = cpu["report"]
-        result["roofline"] = roofline(cpu["visit_mean"], cpu["cand_mean"], "oracle SAH tree on this run's CPU sample")
         result["speedup_vs_cpu"] = value / cpu["report"]["value"]
-    elif rank == 0:
-        # no CPU leg (N > 1, or --no-cpu): V and C of the same workload from the committed N=1 run
-        ref = ROOFLINE_REF.get(args.workload) if (args.photons, args.width) == (
-            WORKLOADS[args.workload]["photons"], WORKLOADS[args.workload]["width"]) else None
-        if ref:
-            result["roofline"] = roofline(ref["V_ref_tree"], ref["C"], ref["source"])
+    else:
+        cpu = None
+    if rank == 0 and world == 1 and st is not None:
+        pmc = None if args.no_pmc else pmc_passes(args)
+        # the counter pass and the PMC passes run iteration 0: hold its bytes to timed iteration 0's
+        # HIP-event launch time (the average over the timed launches is gather_kernel_ms)
+        result["roofline"] = roofline(st, args, wl, gather_per_step[0], pmc, cpu)
     g.close()
     if rank == 0:
         line = json.dumps(result)
@@ -291,22 +285,112 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(path):
-    """HBM bytes per gather launch from a committed rocprofv3 PMC summary (FETCH_SIZE with the
-    gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md), or None when absent."""
-    if not path or not os.path.exists(path):
+def roofline(st, args, wl, gather_ms, pmc, cpu):
+    """HBM roofline of the tile kernel for one launch of iteration 0 (see the module docstring)."""
+    nseg = max(st["n_segments"], 1)
+    items = (nseg + 63) // 64 * args.split
+    # what the packet algorithm must read / write per launch: every visited node line and staged
+    # beam line (64 B each) of every (packet, subtree) item, the segments (40 B in) per item, the
+    # per-subtree partial sums (12 B out), and the reduce (12 B x split in, 12 B out per segment)
+    alg = 64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + nseg * 12 * (args.split + 1)
+    achieved = alg / (gather_ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+           "kernel": "k_gather_tile (+ k_reduce)", "launch": "iteration 0", "launch_ms": gather_ms,
+           "algorithmic_bytes_per_launch": alg,
+           "algorithmic_model": "64 B x (node visits + beam lines staged) + 52 B x 64 per (packet, subtree) "
+                                "item + 12 B x (split + 1) per segment; counts from this run's counter pass"}
+    if pmc:
+        out["traffic"] = pmc.get("traffic_bytes_per_launch")
+        out["traffic_source"] = pmc.get("source")
+        if out["traffic"]:
+            out["traffic_GBps"] = out["traffic"] / (pmc["kernel_ms"] * 1e-3) / 1e9
+            out["traffic_over_algorithmic"] = out["traffic"] / alg
+        if pmc.get("issue"):
+            out["issue"] = pmc["issue"]
+    if cpu and cpu.get("visit_mean"):
+        # SURVEY.md §8d's reference-tree model (every segment streams its candidates from HBM):
+        # kept for comparison, not a fraction of HBM peak
+        bpe = 32 + 12 + 32 * cpu["visit_mean"] + 40 * cpu["cand_mean"]
+        out["ref_model_bytes_per_estimate"] = bpe
+        out["ref_model_GBps"] = bpe * wl.segments_per_gather() / (gather_ms * 1e-3) / 1e9
+        out["ref_model_V_C"] = [cpu["visit_mean"], cpu["cand_mean"]]
+    return out
+
+
+PMC_PASSES = {
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+    "sq": ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
+           "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"],
+}
+
+
+def pmc_passes(args):
+    """This run's own rocprofv3 PMC passes (one counter group per pass, MI355X_MICROARCH.md
+    §rocprofv3): a child process runs one untimed iteration of the same workload per pass.  Returns
+    per-launch HBM bytes and the SQ issue figures of the tile kernel, or None if rocprofv3 is absent
+    or a pass fails (the bench line then has traffic null)."""
+    import csv
+    import shutil
+
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if not prof:
         return None
-    with open(path) as f:
-        summ = json.load(f)
-    tot = 0.0
-    calls = 0
-    for name, v in summ.items():
-        if name.startswith("k_gather"):
-            if "hbm_read_bytes_corrected" not in v:
-                continue
-            tot += (v["hbm_read_bytes_corrected"] + v.get("hbm_write_bytes", 0.0)) * v["calls"]
-            calls = max(calls, v["calls"])  # every gather launches each of its kernels once
-    return tot / calls if calls else None
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload, "--steps", "1",
+             "--warmup", "0", "--photons", str(args.photons), "--width", str(args.width), "--height",
+             str(args.height), "--kernel", str(args.kernel), "--split", str(args.split), "--radius", str(args.radius)]
+    vals, durs = {}, []
+    tmp = tempfile.mkdtemp(prefix="bre_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for name, ctrs in PMC_PASSES.items():
+        d = os.path.join(tmp, name)
+        cmd = [prof, "--pmc", *ctrs, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", *child]
+        try:
+            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150)
+        except subprocess.TimeoutExpired:
+            return None
+        if r.returncode != 0:
+            return None
+        cc = kt = None
+        for root_, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    cc = os.path.join(root_, f)
+                if f.endswith("kernel_trace.csv"):
+                    kt = os.path.join(root_, f)
+        if not cc:
+            return None
+        for row in csv.DictReader(open(cc)):
+            if "k_gather_tile" in row["Kernel_Name"]:
+                vals[row["Counter_Name"]] = vals.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+        if kt and not durs:
+            for row in csv.DictReader(open(kt)):
+                if "k_gather_tile" in row["Kernel_Name"]:
+                    durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
+    shutil.rmtree(tmp, ignore_errors=True)
+    if not durs or "FETCH_SIZE" not in vals:
+        return None
+    # FETCH_SIZE / WRITE_SIZE in KB; gfx950 FETCH_SIZE reads half the bytes of wide streaming reads
+    traffic = vals["FETCH_SIZE"] * 1024 * 2 + vals.get("WRITE_SIZE", 0.0) * 1024
+    res = {"traffic_bytes_per_launch": traffic, "kernel_ms": float(np.mean(durs)),
+           "source": "this run's rocprofv3 --pmc passes (1 iteration, iteration 0: the largest radius)"}
+    clocks = vals.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    if clocks > 0 and vals.get("SQ_WAVE_CYCLES"):
+        wc = vals["SQ_WAVE_CYCLES"]
+        res["issue"] = {
+            "valu_issue_frac": vals["SQ_INSTS_VALU"] / (CUS * SIMDS / 2.0 * clocks),
+            "lds_busy_frac": vals.get("SQ_LDS_IDX_ACTIVE", 0.0) / (CUS * clocks),
+            "wait_any_frac": vals.get("SQ_WAIT_ANY", 0.0) / wc,
+            "wait_inst_any_frac": vals.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+            "wait_inst_lds_frac": vals.get("SQ_WAIT_INST_LDS", 0.0) / wc,
+            "valu_active_frac_of_wave_cycles": vals.get("SQ_ACTIVE_INST_VALU", 0.0) / wc,
+            "SQ_INSTS_VALU": vals["SQ_INSTS_VALU"], "SQ_INSTS_LDS": vals.get("SQ_INSTS_LDS"),
+            "clocks": clocks,
+            "model": "VALU peak = 256 CU x 4 SIMD-32 / 2 clocks per wave64 instruction; LDS busy = "
+                     "SQ_LDS_IDX_ACTIVE / (256 x clocks); clocks = GRBM_GUI_ACTIVE / 8 XCDs",
+        }
+    return res
 
 
 class SceneWorkload:
@@ -314,7 +398,7 @@ class SceneWorkload:
     sigma_s 0.5, g 0); c3/c5 the same box filled with a 64^3 GridDensityMedium of seeded value-noise
     smoke (sigma_a 0.5, sigma_s 4.5, g 0.7); c4 the fog at 2048^2 with 20M photons."""
 
-    def __init__(self, args, bre, g, frame, rank, world):
+    def __init__(self, args, bre, g, frame, shard_rank, shard_count):
         import torch
 
         sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
@@ -326,10 +410,9 @@ class SceneWorkload:
         else:
             self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
-        g.set_shard(rank, world)
+        g.set_shard(shard_rank, shard_count)
         self.ld = frame.accum
         self.scratch = torch.zeros_like(self.ld)
-        self.world = world
         self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "
                      f"{'grid-density smoke' if preset['medium'] == 'smoke' else 'homogeneous fog'}; photons and "
                      "camera paths traced on the GPU)")
@@ -355,45 +438,38 @@ class SceneWorkload:
     def diagnostics(self):
         import torch
 
-        it = 0
-        self.step(it, None, scratch=True)
+        self.step(0, None, scratch=True)
         self.g.synchronize()
         torch.cuda.synchronize()
         st = self.g.stats()
-        self.R0 = self.radius(it)
         return {"beams_per_iteration": st["n_beams"], "photon_pass_ms": st["photon_ms"], "bvh_build_ms": st["build_ms"],
                 "camera_pass_ms": st["camera_ms"], "gather_ms_iter0": st["gather_ms"]}
 
     def segments_per_gather(self):
         return self.last_nseg
 
-    def cpu_beams(self):
-        self.g.trace_photons(self.scene, self.args.photons, 0, self.args.max_depth, self.radius(0))
-        return self.g.get_beams()
-
-    def cpu_segments(self):
-        self.g.camera_pass(self.scene, self.W, self.H, 0, self.args.max_depth, True, True)
+    def cpu_inputs(self, it):
+        """Beams and camera segments of iteration `it` (GPU-traced: bit-exact with the oracle's
+        photon and camera passes, tests/test_photon_gpu.py, tests/test_camera_gpu.py)."""
+        R = self.radius(it)
+        self.g.trace_photons(self.scene, self.args.photons, it, self.args.max_depth, R)
+        beams = self.g.get_beams()
+        self.g.camera_pass(self.scene, self.W, self.H, it, self.args.max_depth, True, True)
         s = self.g.get_segments()
-        return {k: s[k] for k in ("o", "p", "d", "tmax", "pixel")}
+        return beams, {k: s[k] for k in ("o", "p", "d", "tmax", "pixel")}, R
 
-    def cpu_radius(self):
-        return self.radius(0)
-
-    def default_profile(self):
-        if self.name != "c2":
-            return None
-        return os.path.join(ROOT, "profiles", "r09", "profile_summary.json")
-
-    def config(self):
+    def config(self, world):
         a = self.args
         med = ("homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)" if WORKLOADS[self.name]["medium"] == "fog" else
                f"GridDensityMedium smoke {a.grid_n}^3 (sigma_a 0.5, sigma_s 4.5, g 0.7)")
-        film = f"{a.width}x{a.height} per GPU" if a.scaling == "weak" else f"{a.width}x{a.height} split over the GPUs"
+        film = (f"{a.width}x{a.height} split by 16x16 tiles over the GPUs" if a.scaling == "strong" else
+                f"{a.width}x{a.height} per GPU")
         return {"workload": f"{self.name.upper()}: Cornell box + {med}, {a.photons / 1e6:g}M photons/iteration, "
                             f"{film}, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
                 "photons_per_iteration": a.photons, "image": [self.W, self.H], "iterations_timed": a.steps,
-                "parallelism": f"image-tiles x{self.world}, photons traced on every rank",
-                "kernel": KERNEL_NAMES[a.kernel], "leaf_size": a.leaf_size, "split": a.split,
+                "parallelism": f"image tiles x{world} ({a.scaling} scaling), photons traced on every rank, "
+                               "one RCCL gather of the owned-pixel bands per written image",
+                "kernel": KERNEL_NAMES.get(a.kernel, str(a.kernel)), "split": a.split,
                 "prefilter": bool(a.prefilter), "sort_segments": bool(a.sort_segments)}
 
 
@@ -402,17 +478,17 @@ class SyntheticWorkload:
 
     name = "synthetic"
 
-    def __init__(self, args, bre, g, frame, rank, world, dev):
+    def __init__(self, args, bre, g, frame, dev):
         import torch
 
         synth = importlib.import_module("beam-radiance-estimate-pbrt_amd.synth")
-        self.args, self.g, self.frame, self.world = args, g, frame, world
+        self.args, self.g, self.frame = args, g, frame
         self.beams = synth.fog_beams(args.beams, seed=12345, radius=args.radius)
         pixels = frame.pixels
         if args.segment_kind == "camera":
             self.segs = synth.camera_segments(frame.w, frame.h, seed=777, pixels=pixels)
         else:  # incoherent secondary segments, one per owned pixel
-            self.segs = synth.bounce_segments(len(pixels), seed=778 + rank)
+            self.segs = synth.bounce_segments(len(pixels), seed=778)
             self.segs["pixel"] = pixels.astype(np.int32)
         self.nseg = int(self.segs["tmax"].shape[0])
         self.dB = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in self.beams.items()}
@@ -441,71 +517,84 @@ class SyntheticWorkload:
     def segments_per_gather(self):
         return self.nseg
 
-    def cpu_beams(self):
-        return self.beams
+    def cpu_inputs(self, it):
+        return self.beams, self.segs, self.args.radius
 
-    def cpu_segments(self):
-        return self.segs
-
-    def cpu_radius(self):
-        return self.args.radius
-
-    def default_profile(self):
-        return os.path.join(ROOT, "profiles", "r02", "profile_summary.json")
-
-    def config(self):
+    def config(self, world):
         a = self.args
-        return {"workload": "C2 synthetic-fog: 1M-photon beam set, 512x512 camera segments per GPU, R=0.01",
+        return {"workload": "synthetic-fog: 1M-photon beam set, one camera segment per pixel, R=0.01",
                 "beams": a.beams, "segments_per_gpu": self.nseg, "image": [self.frame.w, self.frame.h],
-                "parallelism": f"image-tiles x{self.world}, beams replicated", "kernel": KERNEL_NAMES[a.kernel],
-                "leaf_size": a.leaf_size, "split": a.split, "prefilter": bool(a.prefilter)}
+                "parallelism": f"image tiles x{world}, beams replicated", "kernel": KERNEL_NAMES.get(a.kernel),
+                "split": a.split, "prefilter": bool(a.prefilter)}
 
 
-def cpu_baseline(beams, segs, R, target_s, name):
+def cpu_baseline(wl, args, gather_per_step):
     """Oracle = CPU restatement of the reference algorithm (not pbrt itself: the reference build was
-    denied).  SAH build single-threaded (as photonbeambvh.cpp:232), gather on all
-    available host threads over 256-segment chunks pulled dynamically (ParallelFor2D-like)."""
+    denied).  For the first and the last timed iteration: the SAH build single-threaded
+    (as photonbeambvh.cpp:232), then the gather of a random sample of that iteration's segments on
+    every host thread this process may use (256-segment chunks pulled dynamically, like
+    ParallelFor2D, parallel.cpp:247-299) and on 1 thread.  value = 1 / the mean over the sampled
+    iterations of the seconds per estimate (all threads)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import load_oracle
 
     ora = load_oracle()
-    threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
-    t = time.perf_counter()
-    bvh = ora.build(beams)
-    build_s = time.perf_counter() - t
-    n = segs["tmax"].shape[0]
-    rng = np.random.default_rng(2024)
-    perm = rng.permutation(n)
+    threads = len(os.sched_getaffinity(0))
+    iters = sorted({0, args.steps - 1}) if wl.name != "synthetic" else [0]
+    per_it, visit, cand = [], [], []
+    for it in iters:
+        beams, segs, R = wl.cpu_inputs(it)
+        t = time.perf_counter()
+        bvh = ora.build(beams)
+        build_s = time.perf_counter() - t
+        n = segs["tmax"].shape[0]
+        perm = np.random.default_rng(2024 + it).permutation(n)
 
-    def take(idx):
-        return {k: np.ascontiguousarray(v[idx]) for k, v in segs.items()}
+        def take(idx):
+            return {k: np.ascontiguousarray(v[idx]) for k, v in segs.items()}
 
-    # calibrate on a small sample, then size the timed sample to ~target_s
-    probe = take(perm[: 4 * threads])
-    t = time.perf_counter()
-    bvh.gather(probe, R, nthreads=threads, chunk=1)
-    dt = max(time.perf_counter() - t, 1e-3)
-    per_seg = dt / probe["tmax"].shape[0]
-    m = int(min(n, max(8 * threads, target_s / per_seg)))
-    sample = take(perm[:m])
-    t = time.perf_counter()
-    out = bvh.gather(sample, R, nthreads=threads, chunk=max(1, min(256, m // (4 * threads) or 1)))
-    gather_s = time.perf_counter() - t
-    bvh.close()
-    nb = beams["radius"].shape[0]
+        def timed(m, nthreads, off=0):
+            smp = take(perm[off:off + m])
+            t = time.perf_counter()
+            out = bvh.gather(smp, R, nthreads=nthreads, chunk=max(1, min(256, m // (4 * nthreads) or 1)))
+            return time.perf_counter() - t, out
+
+        # calibrate, then size the samples: target_s / len(iters) on all threads, a quarter of that on 1
+        dt, _ = timed(4 * threads, threads)
+        per_seg = max(dt, 1e-3) / (4 * threads)
+        tgt = args.cpu_seconds / len(iters)
+        m = int(min(n, max(8 * threads, tgt / per_seg)))
+        g_s, out = timed(m, threads)
+        m1 = int(min(n - m, max(4, 0.25 * tgt / (per_seg * threads))))
+        g1_s, _ = timed(m1, 1, off=m)
+        bvh.close()
+        nb = beams["radius"].shape[0]
+        rec = {"iteration": it, "beams": nb, "sah_build_s": build_s, "segments_all_threads": m,
+               "gather_all_threads_s": g_s, "estimates_per_s_all_threads": m / g_s, "segments_1_thread": m1,
+               "gather_1_thread_s": g1_s, "estimates_per_s_1_thread": m1 / g1_s}
+        if it < len(gather_per_step) and wl.segments_per_gather():
+            rec["gpu_gather_only_estimates_per_s"] = wl.segments_per_gather() / (gather_per_step[it] * 1e-3)
+        per_it.append(rec)
+        visit.append(float(out["visit"].mean()))
+        cand.append(float(out["cand"].mean()))
+    value = 1.0 / float(np.mean([1.0 / r["estimates_per_s_all_threads"] for r in per_it]))
+    value1 = 1.0 / float(np.mean([1.0 / r["estimates_per_s_1_thread"] for r in per_it]))
     return {
         "report": {
-            "value": m / gather_s,
+            "value": value,
             "unit": "estimates/s",
             "cores": threads,
+            "nproc": os.cpu_count(),
             "kind": "port",
-            "sample": f"{m} random camera segments of the {name} workload (iteration 0), gather {gather_s:.1f} s on "
-                      f"{threads} threads against all {nb} beams; SAH build of the {nb} beams took {build_s:.1f} s "
-                      f"(1 thread, not in value)",
-            "sah_build_s": build_s,
+            "value_1_thread": value1,
+            "sample": (f"random camera segments of the {wl.name} workload at iterations {iters} (the first and last "
+                       f"timed iterations), gathered against all of that iteration's beams through the oracle's SAH "
+                       f"tree: {threads} threads (every CPU this process may use; nproc {os.cpu_count()}) and 1 thread; "
+                       f"value = 1 / mean seconds per estimate over those iterations"),
+            "per_iteration": per_it,
         },
-        "visit_mean": float(out["visit"].mean()),
-        "cand_mean": float(out["cand"].mean()),
+        "visit_mean": float(np.mean(visit)),
+        "cand_mean": float(np.mean(cand)),
     }
 
 

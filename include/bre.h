@@ -63,27 +63,24 @@ typedef enum bre_status {
 typedef enum bre_option {
     BRE_OPT_COUNTERS = 1,    /* 0/1: per-segment candidate / contribution / node-visit counting */
     BRE_OPT_TIMING = 2,      /* 0/1: HIP-event timing of build and gather kernels (bre_stats ms) */
-    BRE_OPT_KERNEL = 3,      /* 0 = auto (default): kernel 4 on a tree of BRE_OPT_TILE_LEAF-beam leaf
-                                tiles, with the packet bundle reject (fastest measured at C2).
-                                1 = depth-first wave-packet traversal, 2 = thread-per-segment,
-                                3 = packet-proxy traversal with incoherent / overflowing packets
-                                handed to kernel 1 on the device, 4 = depth-first traversal over
-                                leaf tiles (BRE_OPT_LEAF_SIZE) with wavefront-compacted pair queues,
-                                5 = capsule-chunk index, 6 = hand-over: kernel 3 on the
-                                BRE_OPT_LEAF_SIZE (<= 4) tree, kernel 4 on a second tree of
-                                BRE_OPT_TILE_LEAF-beam tiles for the packets kernel 3 hands over.
-                                Every kernel gives the same pair contributions. */
+    BRE_OPT_KERNEL = 3,      /* 0 = the production gather (default): wave-packet traversal over a tree
+                                of BRE_OPT_TILE_LEAF-beam leaf tiles, packet bundle reject, per-lane
+                                separable prefilter, wavefront-compacted exact stage.
+                                4 = the same kernel on a tree of BRE_OPT_LEAF_SIZE-beam leaves,
+                                2 = thread-per-segment traversal (an independent cross-check),
+                                5 = capsule-chunk index.  Values 1, 3 and 6 (round-1 kernels) are
+                                rejected.  Every kernel gives the same pair contributions. */
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..64 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
-    BRE_OPT_SPLIT = 6,       /* kernels 1/3: BVH subtrees per segment packet, power of two 1..64 (default 8) */
-    BRE_OPT_PREFILTER = 7,   /* kernels 1/3: 0/1 conservative line-distance reject before the exact
+    BRE_OPT_SPLIT = 6,       /* kernels 0/4: BVH subtrees per segment packet, power of two 1..64 (default 8) */
+    BRE_OPT_PREFILTER = 7,   /* kernels 0/4/5: 0/1 conservative line-distance rejects before the exact
                                 closest-point code (default 1; results are identical either way) */
     BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles t (the reference's
                                 camera-pass tiles, photonbeam.cpp:345-347) with t % count == rank */
     BRE_OPT_SHARD_COUNT = 9, /* camera pass: number of image-tile shards (default 1 = all tiles).
                                 Set the count before the rank.  Per-pixel results do not depend on
                                 the sharding, so summing the shards' Ld gives the 1-shard image. */
-    BRE_OPT_TILE_LEAF = 10,  /* kernels 0 / 6: beams per leaf tile of the kernel-4 tree, 1..64
+    BRE_OPT_TILE_LEAF = 10,  /* kernel 0: beams per leaf tile of its tree, 1..64
                                 (default 64); applies at the next build */
     BRE_OPT_CHUNK_LEN = 11,  /* kernel 5: chunk length in units of E/100, E = (R + r)(1 + 1e-3) + margin
                                 (25..100000, default 400) */
@@ -148,8 +145,14 @@ bre_status bre_set_beams_device(bre_ctx *ctx, int64_t n, const float *d_start_xy
    (ray.tMax); seg_pixel: int32[nseg], pixel index in [0, npix).
    accum_rgb: float[3*npix], accumulated (+=) like PhotonBeamPixel::Ld (may be NULL).
    seg_rgb: float[3*nseg] per-segment sums, overwritten (may be NULL).
-   seg_counts: int32[2*nseg] per-segment {C candidates, contributions} (may be NULL; needs
-   BRE_OPT_COUNTERS=1).  beam_radius_cur: the integrator's currentBeamRadius R_cur.
+   seg_counts: int32[2*nseg] per-segment {C candidates, contributions} (may be NULL).  With
+   BRE_OPT_COUNTERS=1 both are counted (C by an extra box test of every visited beam); without it
+   the production kernel counts the contributions alone, with its own control flow, and C = -1.
+   beam_radius_cur: the integrator's currentBeamRadius R_cur.
+   Device errors (a traversal-stack overflow: BRE_ERR_STATE; a seg_pixel outside [0, npix):
+   BRE_ERR_INVALID_ARG) are never silent: an asynchronous call reports them at the context's next
+   synchronising call (bre_synchronize, bre_gather, bre_trace_photons, bre_camera_pass, bre_get_*,
+   bre_render*).
    bre_gather takes host pointers (PCIe copies in and out, synchronous); bre_gather_device
    takes device pointers and is asynchronous on the context's stream. */
 bre_status bre_gather(bre_ctx *ctx, int64_t nseg, const float *seg_o_xyz, const float *seg_p_xyz,
@@ -191,6 +194,12 @@ bre_status bre_camera_pass(bre_ctx *ctx, const bre_scene *scene, int32_t width, 
 /* Gather the context's camera segments against its beam set: bre_gather_device on them, adding
    into d_accum_rgb (device float[3*W*H] of the last camera pass).  Asynchronous. */
 bre_status bre_gather_camera(bre_ctx *ctx, float beam_radius_cur, float *d_accum_rgb);
+/* bre_gather_camera with per-segment outputs in the camera-pass order of bre_get_segments:
+   d_seg_rgb (device float[3*n], may be NULL), d_seg_counts (device int32[2*n], may be NULL; as
+   bre_gather's seg_counts).  The gather itself runs exactly as in bre_gather_camera (the same
+   coherence order and kernel instantiation); only the outputs are scattered back.  Asynchronous. */
+bre_status bre_gather_camera_segments(bre_ctx *ctx, float beam_radius_cur, float *d_accum_rgb, float *d_seg_rgb,
+                                      int32_t *d_seg_counts);
 /* Copy the camera segments back (tests): xyz arrays, tmax, pixel index and path depth. */
 bre_status bre_get_segments(bre_ctx *ctx, int64_t capacity, float *o_xyz, float *p_xyz, float *d_xyz, float *tmax,
                             int32_t *pixel, int32_t *depth, int64_t *n_segments);
@@ -209,8 +218,8 @@ bre_status bre_render(bre_ctx *ctx, const bre_scene *scene, const bre_render_par
    iter + 1 == end_iteration or (iter + 1) % write_frequency == 0, the image L = Ld / (iter + 1)
    (host float[3*W*H], row-major from the top row, valid only during the call) is handed to
    `on_image(iter, L, user)`, where the reference calls Film::SetImage + Film::WriteImage.
-   write_frequency <= 0 means "only at the end" (the reference's default 1 << 31 wraps to INT_MIN,
-   which never divides iter + 1).  A non-zero return from on_image stops the render with
+   As in the reference, a negative write_frequency -k also fires every k iterations; INT32_MIN (the
+   reference's default 1 << 31 after wrapping) never divides iter + 1, and 0 means "only at the end".  A non-zero return from on_image stops the render with
    BRE_ERR_STATE.  on_image may be NULL. */
 typedef int (*bre_image_fn)(int32_t iteration, const float *image_rgb, void *user);
 bre_status bre_render_progressive(bre_ctx *ctx, const bre_scene *scene, const bre_render_params *params,

@@ -79,7 +79,7 @@ typedef struct bre_render_params {
     int32_t iterations;             /* "iterations" (default 64) */
     int32_t start_iteration;        /* "startiteration" (default 0) */
     int32_t end_iteration;          /* "enditeration" (default = iterations) */
-    int64_t photons_per_iteration;  /* "photonsperiteration" */
+    int64_t photons_per_iteration;  /* "photonsperiteration"; <= 0: width * height (photonbeam.h:37-39) */
     int32_t max_depth;              /* "maxdepth" (default 5) */
     int32_t render_surfaces;        /* "rendersurfaces" (default 1) */
     int32_t render_media;           /* "rendermedia" (default 1) */

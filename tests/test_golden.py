@@ -40,18 +40,23 @@ def test_oracle_reproduces_golden(gold, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", [1, 2, 3])
-def test_gpu_matches_golden(gold, bre, kernel):
+@pytest.mark.parametrize("kernel,counters", [(0, False), (0, True), (4, False), (2, False), (2, True)])
+def test_gpu_matches_golden(gold, bre, kernel, counters):
+    """(0, False) is the production configuration: the timed instantiation, contributions counted
+    by its own control flow (candidates reported as -1)."""
     s = segs_of(gold)
     accum = np.zeros((1024, 3), np.float32)
-    with bre.BeamGather(0, counters=True, kernel=kernel) as g:
+    with bre.BeamGather(0, counters=counters, kernel=kernel) as g:
         b = beams_of(gold)
         g.set_beams(b["start"], b["end"], b["radius"], b["power"])
         out = g.gather(s["o"], s["p"], s["d"], s["tmax"], s["pixel"], R=float(gold["R"][0]), npix=1024,
                        accum=accum, counts=True)
-    assert np.array_equal(out["counts"][:, 0], gold["cand"])
+    if counters:
+        assert np.array_equal(out["counts"][:, 0], gold["cand"])
+    else:
+        assert (out["counts"][:, 0] == -1).all()
     assert np.array_equal(out["counts"][:, 1], gold["contrib"])
     scale = np.maximum(np.abs(gold["seg_rgb"]).max(axis=1, keepdims=True), 1e-30)
     assert (np.abs(out["seg_rgb"] - gold["seg_rgb"]) / scale).max() <= 1e-5
     rel_l2 = np.linalg.norm(accum - gold["accum"]) / np.linalg.norm(gold["accum"])
-    assert rel_l2 <= 1e-3  # north-star image tolerance (observed ~1e-7)
+    assert rel_l2 <= 1e-5  # summation order only (observed ~1e-7); north star 1e-3

@@ -26,26 +26,27 @@ def _rel_l2(a, b):
     return float(np.sqrt(((a.astype(np.float64) - b) ** 2).sum()) / max(den, 1e-300))
 
 
-@pytest.fixture(scope="module")
-def ctxs(bre):
-    out = {}
-    for k in (1, 2):
-        out[k] = bre.BeamGather(0, counters=True, kernel=k)
-    yield out
-    for c in out.values():
-        c.close()
+KERNELS = [0, 2, 4]
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 6])
+def _production_counts(bre, beams, segs, R, **kw):
+    """The production configuration (kernel 0, counters OFF: the timed instantiation), with the
+    contributions counted by its own control flow."""
+    with bre.BeamGather(0, counters=False, kernel=0, **kw) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        return g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("leaf", [1, 4, 8, 64])
 def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
-    if kernel == 3 and leaf > 4:
-        pytest.skip("kernel 3 needs leaf clusters <= 4 (tested in test_kernel3_rejects_large_leaves)")
     beams = synth.fog_beams(3000, seed=12345)
     segs = synth.camera_segments(48, 40, seed=777)
     R = 0.01
     ref = oracle.build(beams).gather(segs, R)
     with bre.BeamGather(0, counters=True, kernel=kernel, leaf_size=leaf) as g:
+        if kernel == 0:
+            g.set_option(bre.OPT_TILE_LEAF, leaf)
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
         out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, counts=True)
         st = g.stats()
@@ -56,7 +57,7 @@ def test_camera_segments_match_oracle(bre, synth, oracle, kernel, leaf):
     assert st["contributions"] == int(ref["contrib"].sum())
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 6])
+@pytest.mark.parametrize("kernel", KERNELS)
 def test_bounce_segments_match_oracle(bre, synth, oracle, kernel):
     beams = synth.fog_beams(3000, seed=99)
     segs = synth.bounce_segments(3000, seed=5)
@@ -158,7 +159,7 @@ def test_axis_aligned_rays_and_degenerate_segments(bre, oracle):
     ref = oracle.build(beams).gather(segs, 0.02)
     with bre.BeamGather(0, counters=True) as g:
         g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        for k in (0, 1, 2, 3, 4, 6):
+        for k in KERNELS:
             g.set_option(bre.OPT_KERNEL, k)  # the tree shape follows the kernel: rebuild
             g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
             out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.02, counts=True)
@@ -225,7 +226,7 @@ def test_deterministic_per_segment(bre, synth):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 3, 4, 6])
+@pytest.mark.parametrize("kernel", [0, 4])
 @pytest.mark.parametrize("split", [1, 2, 8, 64])
 def test_subtree_split_matches_oracle(bre, synth, oracle, split, kernel):
     beams = synth.fog_beams(4000, seed=51)
@@ -241,8 +242,9 @@ def test_subtree_split_matches_oracle(bre, synth, oracle, split, kernel):
 
 @pytest.mark.parametrize("kind", ["camera", "bounce", "long"])
 def test_prefilter_changes_no_bit(bre, synth, kind):
-    """The conservative line-distance reject must not drop any contributing pair: outputs with and
-    without it are bit-identical, on coherent, incoherent and long-beam / large-radius inputs."""
+    """The conservative line-distance rejects must not drop any contributing pair: outputs with and
+    without them are bit-identical (same queue order), on coherent, incoherent and long-beam /
+    large-radius inputs, for the counting and the production instantiations."""
     if kind == "long":
         beams = synth.fog_beams(6000, seed=61, radius=0.05, mean_length=0.8)
         segs = synth.bounce_segments(6000, seed=62)
@@ -251,20 +253,17 @@ def test_prefilter_changes_no_bit(bre, synth, kind):
         beams = synth.fog_beams(20000, seed=63)
         segs = synth.camera_segments(64, 64, seed=64) if kind == "camera" else synth.bounce_segments(4096, seed=65)
         R = 0.01
-    outs = []
-    for k, pf in ((1, False), (1, True), (3, False), (3, True), (4, False), (4, True), (0, False), (0, True)):
-        with bre.BeamGather(0, counters=True, kernel=k, prefilter=pf) as g:
-            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-            outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True))
-    assert np.array_equal(outs[0]["seg_rgb"], outs[1]["seg_rgb"])
-    assert np.array_equal(outs[0]["counts"], outs[1]["counts"])
-    # kernel 3 visits beams in a different order: same sets, sums equal to rounding
-    for o in outs[2:]:
-        assert np.array_equal(outs[0]["counts"], o["counts"])
-        assert _seg_close(o["seg_rgb"], outs[0]["seg_rgb"]) <= SEG_RTOL
-    assert np.array_equal(outs[2]["seg_rgb"], outs[3]["seg_rgb"])
-    assert np.array_equal(outs[4]["seg_rgb"], outs[5]["seg_rgb"])
-    assert np.array_equal(outs[6]["seg_rgb"], outs[7]["seg_rgb"])
+    outs = {}
+    for counters in (True, False):
+        for pf in (False, True):
+            with bre.BeamGather(0, counters=counters, kernel=0, prefilter=pf) as g:
+                g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+                outs[counters, pf] = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True)
+    ref = outs[True, True]
+    for key, o in outs.items():
+        assert np.array_equal(o["seg_rgb"], ref["seg_rgb"]), key
+        assert np.array_equal(o["counts"][:, 1], ref["counts"][:, 1]), key
+    assert np.array_equal(outs[True, False]["counts"], ref["counts"])
 
 
 @pytest.mark.parametrize("offset", [0.0, 37.5, -250.0])
@@ -303,12 +302,101 @@ def test_prefilters_at_the_threshold(bre, oracle, offset):
         assert np.array_equal(out["counts"][:, 0], ref["cand"]), k
         assert np.array_equal(out["counts"][:, 1], ref["contrib"]), k
         assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    prod = _production_counts(bre, beams, segs, float(R))
+    assert np.array_equal(prod["counts"][:, 1], ref["contrib"])
+    assert _seg_close(prod["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+
+
+@pytest.mark.parametrize("kind", ["threshold", "dense", "axis"])
+def test_production_kernel_pair_exact(bre, synth, oracle, kind):
+    """The timed instantiation (kernel 0, counters off) per segment against the oracle: exact
+    contribution counts through its own control flow, sums to rounding, and bit-identical to the
+    counting instantiation (same queue order)."""
+    rng = np.random.default_rng(7)
+    if kind == "dense":
+        beams = synth.fog_beams(5000, seed=71, radius=0.03, mean_length=0.7)
+        segs = synth.bounce_segments(3000, seed=72)
+        R = 0.04
+    elif kind == "axis":
+        beams = synth.fog_beams(6000, seed=81, radius=0.03, mean_length=0.6)
+        segs = synth.bounce_segments(2500, seed=82)
+        segs["d"][::97] = np.array([0.0, 0.0, 1.0], np.float32)  # axis-parallel rays (infinite 1/d)
+        segs["p"][::97] = segs["o"][::97] + segs["tmax"][::97, None] * segs["d"][::97]
+        R = 0.04
+    else:
+        n = 3000
+        Rf, r = np.float32(0.02), np.float32(0.01)
+        o = rng.random((n, 3), np.float32)
+        d = rng.normal(size=(n, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        p = (o + d * np.float32(0.5)).astype(np.float32)
+        e = np.cross(d, rng.normal(size=(n, 3))).astype(np.float32)
+        e /= np.linalg.norm(e, axis=1, keepdims=True)
+        f = np.cross(d, e).astype(np.float32)
+        eps = rng.uniform(-1e-3, 1e-3, n).astype(np.float32)
+        c = (o + d * np.float32(0.25) + f * ((Rf + r) * (1 + eps))[:, None]).astype(np.float32)
+        beams = {"start": (c - e * np.float32(0.3)).astype(np.float32), "end": (c + e * np.float32(0.3)).astype(np.float32),
+                 "radius": np.full(n, r, np.float32), "power": rng.random((n, 3), np.float32)}
+        segs = {"o": o, "p": p, "d": d, "tmax": np.full(n, 0.5, np.float32)}
+        R = float(Rf)
+    ref = oracle.build(beams).gather(segs, R)
+    prod = _production_counts(bre, beams, segs, R)
+    assert (prod["counts"][:, 0] == -1).all()
+    assert np.array_equal(prod["counts"][:, 1], ref["contrib"])
+    assert _seg_close(prod["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    with bre.BeamGather(0, counters=True, kernel=0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        cnt = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True)
+    assert np.array_equal(cnt["counts"][:, 0], ref["cand"])
+    assert np.array_equal(cnt["seg_rgb"], prod["seg_rgb"])
+
+
+@pytest.mark.parametrize("kernel", [0, 2])
+def test_stack_overflow_is_an_error_without_counters(bre, synth, kernel):
+    """A traversal-stack overflow drops contributions: it must surface as BRE_ERR_STATE at the next
+    synchronising call with the default options (counters off), and the context stays usable."""
+    beams = synth.fog_beams(20000, seed=71, mean_length=0.4)
+    segs = synth.camera_segments(48, 32, seed=72)
+    with bre.BeamGather(0, kernel=kernel, split=1) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        g.set_option(101, 2)  # internal: a 2-entry traversal stack
+        with pytest.raises(bre.BreError) as ei:
+            g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)
+        assert ei.value.status == 4  # BRE_ERR_STATE
+        g.set_option(101, 0)
+        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)  # sticky flag was cleared
+        assert out["seg_rgb"].any()
+
+
+def test_device_pixel_error_reported_at_synchronize(bre, synth):
+    """bre_gather_device is asynchronous: a bad seg_pixel is reported by the next synchronising call."""
+    import torch
+
+    beams = synth.fog_beams(3000, seed=5)
+    segs = synth.camera_segments(16, 16, seed=6)
+    segs["pixel"][7] = 10_000
+    dseg = {k: torch.from_numpy(v).cuda().contiguous() for k, v in segs.items()}
+    with bre.BeamGather(0) as g:
+        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+        acc = torch.zeros((256, 3), dtype=torch.float32, device="cuda")
+        g.gather_device(dseg["o"], dseg["p"], dseg["d"], dseg["tmax"], dseg["pixel"], 0.01, 256, accum=acc)
+        with pytest.raises(bre.BreError) as ei:
+            g.synchronize()
+        assert ei.value.status == 1  # BRE_ERR_INVALID_ARG
+        g.synchronize()  # cleared
+
+
+def test_removed_kernels_are_rejected(bre):
+    with bre.BeamGather(0) as g:
+        for k in (1, 3, 6, 7):
+            with pytest.raises(bre.BreError):
+                g.set_option(bre.OPT_KERNEL, k)
 
 
 @pytest.mark.parametrize("leaf", [16, 64])
 def test_kernel4_dense_incoherent_is_deterministic(bre, synth, oracle, leaf):
-    """Kernel 4's compaction queue and LDS accumulators on a dense, incoherent set (long beams,
-    large radius: many candidates per lane): exact sets, sums to rounding, bit-identical reruns."""
+    """The tile kernel's compaction queue and LDS accumulators on a dense, incoherent set (long
+    beams, large radius: many candidates per lane): exact sets, sums to rounding, bit-identical reruns."""
     beams = synth.fog_beams(5000, seed=71, radius=0.03, mean_length=0.7)
     segs = synth.bounce_segments(3000, seed=72)
     ref = oracle.build(beams).gather(segs, 0.04)
@@ -321,76 +409,3 @@ def test_kernel4_dense_incoherent_is_deterministic(bre, synth, oracle, leaf):
     assert np.array_equal(runs[0]["counts"][:, 1], ref["contrib"])
     assert _seg_close(runs[0]["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
     assert np.array_equal(runs[0]["seg_rgb"], runs[1]["seg_rgb"])
-
-
-def test_kernel3_rejects_large_leaves(bre, synth):
-    beams = synth.fog_beams(500)
-    segs = synth.camera_segments(8, 8)
-    with bre.BeamGather(0, kernel=3, leaf_size=8) as g:
-        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        with pytest.raises(bre.BreError):
-            g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01)
-
-
-def test_kernel3_stack_overflow_falls_back_exactly(bre, synth, oracle):
-    """Wide incoherent packets over a deep tree can exhaust kernel 3's LDS stack; kernel 1 then
-    recomputes on the device and the results stay exact."""
-    beams = synth.fog_beams(20000, seed=71, mean_length=0.4)
-    segs = synth.camera_segments(48, 32, seed=72)
-    ref = oracle.build(beams).gather(segs, 0.01)
-    with bre.BeamGather(0, counters=True, kernel=3, split=1, leaf_size=1) as g:
-        g.set_option(101, 70)  # internal: 70-entry stack -> most packets overflow
-        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01, counts=True)
-    assert np.array_equal(out["counts"][:, 0], ref["cand"])
-    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
-    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
-
-
-
-@pytest.mark.parametrize("tile_leaf", [8, 32, 64])
-def test_auto_handover_mixed_packets(bre, synth, oracle, tile_leaf):
-    """Hand-over mode (kernel 6): coherent camera packets stay in kernel 3, incoherent bounce packets
-    go to kernel 4 on the tile tree; one gather over both kinds matches the oracle exactly (sets) and
-    to rounding."""
-    beams = synth.fog_beams(6000, seed=81, mean_length=0.4)
-    cam = synth.camera_segments(32, 32, seed=82)
-    bnc = synth.bounce_segments(2048, seed=83, npix=1024)
-    segs = {k: np.concatenate([cam[k], bnc[k]]) for k in cam}
-    R = 0.012
-    ref = oracle.build(beams).gather(segs, R, npix=1024)
-    accum = np.zeros((1024, 3), np.float32)
-    with bre.BeamGather(0, counters=True, kernel=6) as g:
-        g.set_option(bre.OPT_TILE_LEAF, tile_leaf)
-        g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-        out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R, npix=1024, accum=accum,
-                       counts=True)
-        st = g.stats()
-    assert st["redo_items"] > 0  # the bounce packets were handed over
-    assert np.array_equal(out["counts"][:, 0], ref["cand"])
-    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
-    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
-    assert _rel_l2(accum, ref["accum"]) <= 1e-6
-
-
-@pytest.mark.parametrize("leaf", [16, 32])
-def test_kernel4_leaf_orders_are_bit_identical(bre, synth, oracle, leaf):
-    """Kernel 4's prefilter-first leaf scan (tile_mode 1, default) and box-first scan (0) queue the
-    contributing pairs in the same (leaf, beam, lane) order: same counts, bit-identical sums, and
-    both exact against the oracle (including axis-parallel rays, which take the slab test)."""
-    beams = synth.fog_beams(6000, seed=81, radius=0.03, mean_length=0.6)
-    segs = synth.bounce_segments(2500, seed=82)
-    segs["d"][::97] = np.array([0.0, 0.0, 1.0], np.float32)  # axis-parallel rays (infinite 1/d)
-    segs["p"][::97] = segs["o"][::97] + segs["tmax"][::97, None] * segs["d"][::97]
-    ref = oracle.build(beams).gather(segs, 0.04)
-    outs = []
-    for mode in (0, 1):
-        with bre.BeamGather(0, counters=True, kernel=4, leaf_size=leaf) as g:
-            g.set_option(104, mode)
-            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-            outs.append(g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.04, counts=True))
-    for o in outs:
-        assert np.array_equal(o["counts"][:, 0], ref["cand"])
-        assert np.array_equal(o["counts"][:, 1], ref["contrib"])
-        assert _seg_close(o["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
-    assert np.array_equal(outs[0]["seg_rgb"], outs[1]["seg_rgb"])

@@ -80,7 +80,7 @@ def test_c2_scene_file_is_the_benchmark_scene(pb, sc):
     assert (p.photons_per_iteration, p.max_depth, p.render_surfaces, p.render_media) == (1_000_000, 5, 1, 1)
     assert p.initial_radius == np.float32(0.01) and p.alpha == 0.5
     assert s.film == dict(xres=512, yres=512, scale=1.0, filename="cornell_fog_c2.pfm")
-    assert s.write_frequency == 0  # the reference's default 1 << 31 never divides iter + 1
+    assert s.write_frequency == -2**31  # the reference's default 1 << 31 (INT_MIN): never divides iter + 1
 
 
 def test_c1_scene_file(pb):
