@@ -16,7 +16,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbre.so")
+# BRE_LIBRARY: another build of the same C ABI (profiling ablations, profiles/ablate.sh); the
+# default is the in-tree libbre.so.  There is no CPU fallback either way.
+LIB_PATH = os.environ.get("BRE_LIBRARY") or os.path.join(HERE, "libbre.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "bre.h")
 
 BRE_OK = 0

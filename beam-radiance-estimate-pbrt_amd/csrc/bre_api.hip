@@ -60,7 +60,8 @@ struct bre_ctx {
     int split = 8;
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
-    int occupancy = 8;       // tile kernel register budget (min waves per SIMD): 8 measured best at C2
+    int scan_mode = 0;       // internal: tile kernel scan source (GatherArgs::scan_mode)
+    int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best at C2 (r2)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
@@ -83,7 +84,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial, pcnt;
+    DevMem counters_buf, roots, partial, pcnt, segrec;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // camera pass
@@ -396,6 +397,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.prefilter = c->prefilter;
     a.occupancy = c->occupancy;
     a.stack_cap = c->stack_cap;
+    a.scan_mode = c->scan_mode;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
@@ -417,6 +419,8 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         a.roots = c->roots.as<int32_t>();
         a.partial = c->partial.as<float>();
+        HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)nseg));
+        a.segrec = c->segrec.as<SegRec>();
         if (c->counters || seg_counts) {
             HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
             a.pcnt = c->pcnt.as<int32_t>();
@@ -498,7 +502,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -575,6 +579,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
+    case 106:  // internal: tile kernel scan source, 0 LDS / 1 registers (sweeps)
+        if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "scan mode must be 0 or 1");
+        c->scan_mode = (int)value;
+        return BRE_OK;
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }
 }

@@ -103,6 +103,17 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s);
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 
+// One gathered segment as the tile kernel's exact stage reads it (k_seg_prep): 64 B, one line.
+struct alignas(16) SegRec {
+    float o[3], tmax;   // ray.o, ray.tMax
+    float p[3], mag_a;  // isect.p, |p - o|
+    float au[3];        // (p - o) * (1 / |p - o|)
+    int32_t has_inf;    // some 1 / d_i is infinite (axis-parallel ray)
+    float invs[3];      // 1 / d with infinities replaced by +-FLT_MAX
+    float omax;         // max |o_i| + |p - o|
+};
+static_assert(sizeof(SegRec) == 64, "SegRec must be one 64-B line");
+
 struct GatherArgs {
     int64_t nseg;
     const float *o, *p, *d, *tmax;
@@ -124,9 +135,11 @@ struct GatherArgs {
     int split;             // S, power of two <= kMaxSplit
     float *partial;        // [split][nseg][3]
     int32_t *pcnt;         // [split][nseg][2] per-subtree counts (counters / contribution counting)
+    SegRec *segrec;        // [nseg] tile kernel: per-segment records (written by k_seg_prep)
     bool prefilter;
     int occupancy;         // tile kernel register budget: min waves per SIMD (1, 6, 7 or 8)
     int stack_cap;         // traversal stack entries to use (0 = all); tests force an overflow
+    int scan_mode;         // tile kernel scan: 0 tile staged in LDS (default), 1 tile in registers + v_readlane
 };
 
 // capsule-chunk index (bre_chunk.hip)

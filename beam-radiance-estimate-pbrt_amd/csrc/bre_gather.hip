@@ -34,6 +34,14 @@ namespace {
 
 constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 
+// Profiling ablations (compile-time, off in the product; profiles/ablate.sh builds them into
+// separate libraries): BRE_ABLATE 1 = exact stage without the LDS float atomics (plain stores:
+// wrong sums), 2 = no exact stage (queue drained unread), 3 = no prefilter scan (every kept beam's
+// prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf tiles not scanned).
+#ifndef BRE_ABLATE
+#define BRE_ABLATE 0
+#endif
+
 struct Prof {
     unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0;
 };
@@ -192,13 +200,18 @@ __device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float 
 // and packets of incoherent bounce segments share few of them) the exact per-pair code executed
 // under a 64-lane mask is the cost: a wave would run ComputeClosestPoints whenever ANY lane needs
 // it, with a few % of the lanes active.  Per visited leaf tile:
-//   1. its beams are staged in LDS kTileMax at a time in the scan layout below, one beam per lane;
+//   1. lane j loads beam j of the tile and keeps its scan values in REGISTERS (7 VGPRs);
 //   2. the packet bundle test (one beam per lane) drops beams far from every segment of the packet;
-//   3. each lane runs the separable line-distance prefilter on the kept beams; (beam, lane) pairs
-//      that pass are appended to a per-wave LDS ring (ballot + mbcnt);
+//   3. each lane runs the separable line-distance prefilter on the kept beams, the beam's values
+//      broadcast from their lane by v_readlane into SGPRs; (beam, lane) pairs that pass are
+//      appended to a per-wave LDS ring, one 32-bit entry each (ballot + mbcnt);
 //   4. every 64 queued pairs run, one pair per lane with all lanes busy, the reference's box test
-//      on the beam's (group) box, ComputeClosestPoints and the kernel, and add the contribution to
-//      the segment's LDS accumulator.
+//      on the beam's (group) box, ComputeClosestPoints and the kernel, with the segment read back
+//      from its 64-B record (k_seg_prep) through the vector cache, and add the contribution to the
+//      segment's LDS accumulator.
+// r2 profile of the round-1 form (tile staged in LDS, segment fields moved by 14 ds_bpermutes per
+// batch): LDS array busy 60% of the kernel's clocks and 52% of the wave cycles stalled on LDS issue,
+// VALU issue 22%; this form moves ~2.5x fewer LDS instructions.
 // The prefilters only drop pairs with a computed distance >= R + r, which never contribute, and the
 // box test is the reference's own, so the contributing pairs and each pair's value are the
 // reference's; a segment's pairs are summed in queue order (leaf, beam, lane), fixed by the
@@ -206,99 +219,151 @@ __device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float 
 //
 // Separable prefilter.  With t = b0 - o and n = au x bu,
 //   t.n = au.(bu x b0) - bu.(o x au) = au.m0 - bu.q,
-// so per (lane, beam) only two dot products and c = au.bu remain: m0 is staged per beam, q per lane.
+// so per (lane, beam) only two dot products and c = au.bu remain: m0 is held per beam, q per lane.
 // |n|^2 = |au|^2|bu|^2 - c^2 (Lagrange) is bracketed by 0.99999 - c^2 <= |n|^2 <= 1.00001 - c^2
 // (unit vectors to ~1e-7, c to ~5e-7).  The computed t.n is within 1e-5 (bmax + omax) + 1e-6 of
 // the exact one (~2e-6 (bmax + omax) by the float error of the cross and dot products), and the
 // coordinate bound mag of far_from_lines uses tl <= |b0|_1 + |o|_1, so its margins split into a
-// beam part (staged: Ab, Eb) and a lane part (Al, El):
-//   reject  <=>  tn > (Eb + El) + (Ab + Al) * (sqrt(nn_hi) * 1.000001 + 1e-6)
+// beam part (Ab, Eb) and a lane part (Al, El):
+//   reject  <=>  tn > (Eb + El) + (Ab + Al) * nl,   nl = sqrt(nn_hi) * 1.000001 + 1e-6
 // which implies the line-line distance exceeds maxd * 1.0001 + 2 eps with eps >= far_from_lines'
-// eps: the same proof that every reference-computed distance of the pair is >= maxd.  Near-parallel
-// pairs (|n|^2 possibly < 1e-2) and zero-length segments (El = FLT_MAX) are never rejected.
+// eps: the same proof that every reference-computed distance of the pair is >= maxd.  A rejected
+// pair has nn_lo >= 1e-2, so nl > 0.1 and Eb + El < 10 (Eb + El) nl: the single-margin test
+//   reject  <=>  tn > (Ab' + Al') * nl,   Ab' = Ab + 10 Eb,  Al' = Al + 10 El
+// rejects a subset of those pairs (still a proof).  Near-parallel pairs (|n|^2 possibly < 1e-2) and
+// zero-length segments (Al' = FLT_MAX) are never rejected.
 struct ScanLane {
     f3 q;       // o x au
-    float al;   // 2e-5 (omax + 10 |o|_1)
-    float el;   // 1e-5 omax, FLT_MAX for a zero-length segment
+    float al;   // Al' = 2e-5 (omax + 10 |o|_1) + 1e-4 omax;  FLT_MAX for a zero-length segment
 };
 
 __device__ __forceinline__ ScanLane make_scan_lane(const Lane &L) {
     ScanLane S;
     S.q = mk(L.o.y * L.au.z - L.o.z * L.au.y, L.o.z * L.au.x - L.o.x * L.au.z, L.o.x * L.au.y - L.o.y * L.au.x);
     const float o1 = fabsf(L.o.x) + fabsf(L.o.y) + fabsf(L.o.z);
-    S.al = 2e-5f * (L.omax + 10.0f * o1);
-    S.el = L.mag_a == 0.0f ? FLT_MAX : 1e-5f * L.omax;
+    S.al = L.mag_a == 0.0f ? FLT_MAX : 2e-5f * (L.omax + 10.0f * o1) + 1e-4f * L.omax;
     return S;
 }
 
-__device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, f3 bu, f3 m0, float ab, float eb) {
-    const float c = __builtin_fmaf(au.x, bu.x, __builtin_fmaf(au.y, bu.y, au.z * bu.z));
+// The beam side of the scan: bu, m0 = bu x b0 and Ab' (maxd = R + r folded in).
+struct ScanBeam {
+    f3 bu, m0;
+    float ab;
+};
+
+__device__ __forceinline__ ScanBeam make_scan_beam(const BeamV &r, float R) {
+    const float maxd = R + r.radius;
+    ScanBeam B;
+    B.bu = r.bu;
+    B.m0 = mk(r.bu.y * r.b0.z - r.bu.z * r.b0.y, r.bu.z * r.b0.x - r.bu.x * r.b0.z, r.bu.x * r.b0.y - r.bu.y * r.b0.x);
+    const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
+    const float b1 = fabsf(r.b0.x) + fabsf(r.b0.y) + fabsf(r.b0.z);
+    // Ab = maxd 1.0001 + 2e-5 (bmax + 10 |b0|_1) + 2e-6, Eb = 1e-5 bmax + 1e-6
+    B.ab = maxd * 1.0001f + 2e-5f * (bmax + 10.0f * b1) + 2e-6f + 10.0f * (1e-5f * bmax + 1e-6f);
+    return B;
+}
+
+__device__ __forceinline__ float rdl(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// Beam j's scan values, broadcast from lane j's registers by v_readlane (wave-uniform: SGPRs).
+__device__ __forceinline__ ScanBeam scan_beam_of(const ScanBeam &T, int j) {
+    ScanBeam B;
+    B.bu = mk(rdl(T.bu.x, j), rdl(T.bu.y, j), rdl(T.bu.z, j));
+    B.m0 = mk(rdl(T.m0.x, j), rdl(T.m0.y, j), rdl(T.m0.z, j));
+    B.ab = rdl(T.ab, j);
+    return B;
+}
+
+// Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128).
+__device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j) {
+    const float4 a = tile[j][0], b = tile[j][1];
+    ScanBeam B;
+    B.bu = mk(a.x, a.y, a.z);
+    B.ab = a.w;
+    B.m0 = mk(b.x, b.y, b.z);
+    return B;
+}
+
+// Branch-free (no early exit for near-parallel pairs): the beam's values can be read in one go and
+// two beams' tests interleave.  fma(-c, c, 1.00001) > 0 for unit vectors, so nl is never NaN.
+__device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, const ScanBeam &B) {
+    const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
     const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
-    if (!(nn_lo >= 1e-2f)) return false;
-    const float x = __builtin_fmaf(au.x, m0.x, __builtin_fmaf(au.y, m0.y, au.z * m0.z));
-    const float tn = fabsf(__builtin_fmaf(-bu.x, S.q.x, __builtin_fmaf(-bu.y, S.q.y, __builtin_fmaf(-bu.z, S.q.z, x))));
+    const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
+    const float tn =
+        fabsf(__builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x))));
     const float nl = __builtin_amdgcn_sqrtf(__builtin_fmaf(-c, c, 1.00001f)) * 1.000001f + 1e-6f;
-    return tn > __builtin_fmaf(ab + S.al, nl, eb + S.el);
+    return (nn_lo >= 1e-2f) & (tn > (B.ab + S.al) * nl);
 }
 
 constexpr int kTileBlock = 256;  // 4 waves
 constexpr int kQueueCap = 128;   // >= 63 left over + 64 appended by one beam
-constexpr int kTileMax = 32;     // beams staged in LDS at a time (longer leaves go in chunks; 64 costs occupancy)
+constexpr int kRing = 64;        // leaf-base ring: queue entries reference < 64 distinct leaves (see push)
 
 struct TileShared {
-    float4 tile[kTileMax][3];  // staged scan layout of the current leaf chunk: (b0, maxd), (bu, Ab), (m0, Eb)
+    float4 tile[64][2];        // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
     float acc[3][64];          // per-segment RGB accumulators
     int32_t cnt[64];           // per-segment contribution counts (counters / contribution counting)
-    int32_t qb1[kQueueCap];    // prefilter-survivor ring: beam index
-    uint8_t ql1[kQueueCap];    //                          segment lane
+    uint32_t q[kQueueCap];     // prefilter-survivor ring: ring slot << 12 | beam-in-tile << 6 | segment lane
+    int32_t leaf[kRing];       // first beam of the leaf tile each ring slot stands for
     int32_t stk[kStackDepth];
 };
 
-__device__ __forceinline__ float lane_f(float v, int src) { return __shfl(v, src); }
-
 // The exact stage for n queued prefilter survivors (one per lane; all lanes call): the reference's
-// box test on the beam's (group) box, then ComputeClosestPoints + kernel.  The pair's beam line
-// comes from L2 (the staged chunk may already be replaced).
-__device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, int first, int n,
-                                               const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
-                                               float R, const float *__restrict__ sd, int64_t seg0, bool count) {
+// box test on the beam's (group) box, then ComputeClosestPoints + kernel.  The pair's segment comes
+// from its SegRec, the beam line from L2.
+__device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
+                                           const float *__restrict__ sd, int64_t seg0,
+                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
+                                           bool count) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
-    const int e = (first + (on ? lane : 0)) & (kQueueCap - 1);  // FIFO ring
-    const int32_t b = sh.qb1[e];
-    const int sl = sh.ql1[e];
-    const f3 o = mk(lane_f(M.o.x, sl), lane_f(M.o.y, sl), lane_f(M.o.z, sl));
-    const f3 invs = mk(lane_f(M.invs.x, sl), lane_f(M.invs.y, sl), lane_f(M.invs.z, sl));
-    const float tmax = lane_f(M.tmax, sl);
-    const BeamV r = load_beam(recs, b);
+    const uint32_t e = sh.q[(first + (on ? lane : 0)) & (kQueueCap - 1)];  // FIFO ring
+    const int sl = (int)(e & 63u);
+    const int64_t b = (int64_t)sh.leaf[e >> 12] + ((e >> 6) & 63u);
+    // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
+    const float4 *sr = reinterpret_cast<const float4 *>(srec + seg0 + sl);
+    const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
+    const float4 s0 = sr[0], s3 = sr[3], bx = rb[0], by = rb[1];
+    const f3 o = mk(s0.x, s0.y, s0.z);
+    const float tmax = s0.w;
+    const Box6 box{bx.x, bx.y, bx.z, bx.w, by.x, by.y};
     float te;
-    bool hit = on & node_test(r.box, o, invs, tmax, te);
-    const bool inf = __shfl((int)M.has_inf, sl) != 0;
+    bool hit = on & node_test(box, o, mk(s3.x, s3.y, s3.z), tmax, te);
+    const float4 s2 = sr[2];
+    const bool inf = s2.w != 0.f;  // has_inf (integer 1 as float bits: a denormal, never 0)
     if (__ballot(on & inf) != 0ull) {
         if (on & inf) {
-            // the rare axis-parallel ray: its direction is re-read (keeps Lane::d out of registers)
+            // the rare axis-parallel ray: the literal slab test on its exact 1/d
             const int64_t so = seg0 + sl;
             const f3 d = mk(sd[3 * so], sd[3 * so + 1], sd[3 * so + 2]);
             const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
-            hit = slab_test(r.box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
+            hit = slab_test(box, o, inv, inv.x < 0, inv.y < 0, inv.z < 0, tmax, nullptr);
         }
     }
     if (__ballot(hit) == 0ull) return;
-    // the power load is issued ahead of the closest-point arithmetic (most box hits contribute)
+    // phase 2: closest points + kernel (the power load is issued first: most box hits contribute)
     const float4 pv = hit ? pw[b] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const f3 p = mk(lane_f(M.p.x, sl), lane_f(M.p.y, sl), lane_f(M.p.z, sl));
-    const f3 au = mk(lane_f(M.au.x, sl), lane_f(M.au.y, sl), lane_f(M.au.z, sl));
-    const float mag_a = lane_f(M.mag_a, sl);
+    const float4 bz = rb[2], bw = rb[3], s1 = sr[1];
     if (hit) {
-        const float maxd = R + r.radius;  // MaxDistance = currentBeamRadius + beam->radius
+        const float maxd = R + bw.y;  // MaxDistance = currentBeamRadius + beam->radius
         float dist;
-        const bool ok = closest_distance(o, p, au, mag_a, r.b0, r.bu, r.mag_b, dist);
+        const bool ok = closest_distance(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w, mk(by.z, by.w, bz.x),
+                                         mk(bz.y, bz.z, bz.w), bw.x, dist);
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
             const float w = sqrtf(1.0f - rr * rr);
-            atomicAdd(&sh.acc[0][sl], pv.x * w);
-            atomicAdd(&sh.acc[1][sl], pv.y * w);
-            atomicAdd(&sh.acc[2][sl], pv.z * w);
+            if (BRE_ABLATE == 1) {
+                sh.acc[0][sl] = pv.x * w;
+                sh.acc[1][sl] = pv.y * w;
+                sh.acc[2][sl] = pv.z * w;
+            } else {
+                atomicAdd(&sh.acc[0][sl], pv.x * w);
+                atomicAdd(&sh.acc[1][sl], pv.y * w);
+                atomicAdd(&sh.acc[2][sl], pv.z * w);
+            }
             if (count) atomicAdd(&sh.cnt[sl], 1);
         }
     }
@@ -306,14 +371,15 @@ __device__ __forceinline__ void tile_box_exact(TileShared &sh, const Lane &M, in
 
 // COUNT: also box-test every beam of every visited tile and count the candidates (the reference's
 // C), plus traversal statistics; the queue of pairs and hence every sum are the same as without.
-// ccnt (runtime, wave-uniform): count the contributions per segment in the production
+// pcnt (runtime, wave-uniform): count the contributions per segment in the production
 // instantiation, with the production control flow (per-subtree counts in pcnt[.][1]).
-template <bool COUNT, int MINW>
+template <bool COUNT, int MINW, bool SCAN_LDS>
 __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
-    const float *__restrict__ stmax, float R, float *__restrict__ partial, int32_t *__restrict__ pcnt,
-    const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
-    int leaf_size, const int32_t *__restrict__ roots, int S, DevCounters *ctr, int stack_cap, int prefilter) {
+    const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
+    int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+    const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
+    DevCounters *ctr, int stack_cap, int prefilter) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  Blocks b and b+8 share an XCD under the observed round-robin
     // dispatch, so for S >= 8 XCD (b & 7) is given the S/8 consecutive work roots below one depth-3
@@ -349,22 +415,31 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int cand = 0;
     unsigned long long visits = 0;
     Prof pf;
-    int h1 = 0, t1 = 0;  // wave-uniform FIFO ring head / tail
+    int h1 = 0, t1 = 0;        // wave-uniform FIFO ring head / tail
+    int ring_next = 0;         // next leaf-base ring slot
+    int cur_slot = -1;         // ring slot of the current leaf (-1: none yet)
+    int64_t cur_first = 0;     // first beam of the current leaf
 
-    // queue the (beam, lane) survivors of beam j; drain 64 at a time (ring < 128)
-    const auto push = [&](int64_t bj, bool need) {
+    // queue the (beam, lane) survivors of beam j of the current leaf; drain 64 at a time.  A leaf
+    // takes a ring slot at its first push: the < 64 entries left after a drain reference < 64 slots,
+    // all among the last 63 assigned, so a kRing = 64 ring never reuses a slot a live entry holds.
+    const auto push = [&](int j, bool need) {
         const unsigned long long m = __ballot(need);
         if (m == 0ull) return;
+        if (cur_slot < 0) {
+            cur_slot = ring_next;
+            ring_next = (ring_next + 1) & (kRing - 1);
+            if (lane == 0) sh.leaf[cur_slot] = (int32_t)cur_first;
+        }
         if (need) {
             const int pos = (t1 + lanes_below(m)) & (kQueueCap - 1);
-            sh.qb1[pos] = (int32_t)bj;
-            sh.ql1[pos] = (uint8_t)lane;
+            sh.q[pos] = ((uint32_t)cur_slot << 12) | ((uint32_t)j << 6) | (uint32_t)lane;
         }
         t1 += __popcll(m);
         __builtin_amdgcn_wave_barrier();
         if (t1 - h1 >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_box_exact(sh, L, h1, 64, recs, pw, R, sd, seg0, count_c);
+            if (BRE_ABLATE != 2) tile_exact(sh, h1, 64, srec, sd, seg0, recs, pw, R, count_c);
             h1 += 64;
             if (h1 >= 1024) {
                 h1 -= 1024;
@@ -374,92 +449,84 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         }
     };
 
-    // scan one leaf: its beams are staged in LDS kTileMax at a time (scan layout), bundle reject,
-    // then per lane the separable prefilter on the kept beams; survivors queue for the exact stage
+    // scan one leaf tile (<= 64 beams): lane j holds beam j's scan values; bundle reject; per lane the
+    // separable prefilter on the kept beams; survivors queue for the exact stage
     const auto leaf = [&](int32_t c, bool lane_on) {
         const int64_t first = (int64_t)(~c) * leaf_size;
-        const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
+        const int nb = (int)min((int64_t)leaf_size, nvalid - first);
         if (COUNT) {
             ++pf.leaves;
-            pf.beams += cnt;
+            pf.beams += nb;
         }
-        for (int base = 0; base < cnt; base += kTileMax) {
-            const int nb = min(kTileMax, cnt - base);
-            const int64_t tile0 = first + base;
-            __builtin_amdgcn_wave_barrier();
-            // lane j stages beam j: (b0, maxd), (bu, Ab), (m0 = bu x b0, Eb)
+        if (BRE_ABLATE == 4) return;
+        cur_first = first;
+        cur_slot = -1;
+        ScanBeam T;
+        T.bu = T.m0 = mk(0.f, 0.f, 0.f);
+        T.ab = 0.f;
+        bool keep = false;
+        if (lane < nb) {
+            const BeamV r = load_beam(recs, first + lane);
+            T = make_scan_beam(r, R);
+            // packet-level bundle reject (see make_bundle): a beam far from every segment of the
+            // packet is skipped by all lanes
+            keep = !prefilter || !bundle_far(K, r.b0, r.bu, R + r.radius);
+        }
+        const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
+        const unsigned long long km = __ballot(keep) & all;
+        if (SCAN_LDS) {
+            __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
             if (lane < nb) {
-                const BeamV r = load_beam(recs, tile0 + lane);
-                const float maxd = R + r.radius;
-                const f3 m0 = mk(r.bu.y * r.b0.z - r.bu.z * r.b0.y, r.bu.z * r.b0.x - r.bu.x * r.b0.z,
-                                 r.bu.x * r.b0.y - r.bu.y * r.b0.x);
-                const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
-                const float b1 = fabsf(r.b0.x) + fabsf(r.b0.y) + fabsf(r.b0.z);
-                const float ab = maxd * 1.0001f + 2e-5f * (bmax + 10.0f * b1) + 2e-6f;
-                const float eb = 1e-5f * bmax + 1e-6f;
-                sh.tile[lane][0] = make_float4(r.b0.x, r.b0.y, r.b0.z, maxd);
-                sh.tile[lane][1] = make_float4(r.bu.x, r.bu.y, r.bu.z, ab);
-                sh.tile[lane][2] = make_float4(m0.x, m0.y, m0.z, eb);
+                sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, T.ab);
+                sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
             }
             __builtin_amdgcn_wave_barrier();
-            const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
-            // packet-level bundle reject, one beam per lane (see make_bundle): beams far from every
-            // segment of the packet are skipped by all lanes
-            unsigned long long km = all;
-            if (prefilter) {
-                bool keep = false;
-                if (lane < nb) {
-                    const float4 x = sh.tile[lane][0], y = sh.tile[lane][1];
-                    keep = !bundle_far(K, mk(x.x, x.y, x.z), mk(y.x, y.y, y.z), x.w);
-                }
-                km = __ballot(keep) & all;
+        }
+        const auto beam_of = [&](int j) { return SCAN_LDS ? scan_beam_lds(sh.tile, j) : scan_beam_of(T, j); };
+        if (COUNT) {
+            pf.useful += __popcll(km);
+            // every beam of the tile: the reference box test (candidates) and the pairs the
+            // prefilters drop; the queue gets exactly the production survivors, in order
+            for (int j = 0; j < nb; ++j) {
+                bool need = lane_on && ((km >> j) & 1ull);
+                if (prefilter && need) need = !scan_far(SL, L.au, beam_of(j));
+                const Box6 box = load_beam(recs, first + j).box;
+                float te;
+                bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
+                if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
+                cand += hit;
+                pf.rejects += hit & !need;
+                push(j, need);
             }
-            if (COUNT) {
-                pf.useful += __popcll(km);
-                // every beam of the chunk: the reference box test (candidates) and the pairs the
-                // prefilters drop; the queue gets exactly the production survivors, in order
-                for (int j = 0; j < nb; ++j) {
-                    bool need = lane_on && ((km >> j) & 1ull);
-                    if (prefilter && need) {
-                        const float4 y = sh.tile[j][1], z = sh.tile[j][2];
-                        need = !scan_far(SL, L.au, mk(y.x, y.y, y.z), mk(z.x, z.y, z.z), y.w, z.w);
-                    }
-                    const Box6 box = load_beam(recs, tile0 + j).box;
-                    float te;
-                    bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
-                    if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
-                    cand += hit;
-                    pf.rejects += hit & !need;
-                    push(tile0 + j, need);
-                }
-                continue;
-            }
-            if (!prefilter) {
-                for (int j = 0; j < nb; ++j) push(tile0 + j, lane_on);
-                continue;
-            }
-            // two kept beams per step: independent LDS reads and prefilters (ILP), then the
-            // survivors are queued beam by beam in order
-            unsigned long long todo = km;
-            while (todo != 0ull) {
-                const int j1 = __ffsll((long long)todo) - 1;
-                todo &= todo - 1ull;
-                const bool two = todo != 0ull;
-                const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
-                if (two) todo &= todo - 1ull;
-                const float4 y1 = sh.tile[j1][1], z1 = sh.tile[j1][2];
-                const float4 y2 = sh.tile[j2][1], z2 = sh.tile[j2][2];
-                const bool n1 = lane_on && !scan_far(SL, L.au, mk(y1.x, y1.y, y1.z), mk(z1.x, z1.y, z1.z), y1.w, z1.w);
-                const bool n2 = two && lane_on &&
-                                !scan_far(SL, L.au, mk(y2.x, y2.y, y2.z), mk(z2.x, z2.y, z2.z), y2.w, z2.w);
-                push(tile0 + j1, n1);
-                if (two) push(tile0 + j2, n2);
-            }
+            return;
+        }
+        if (!prefilter) {
+            for (int j = 0; j < nb; ++j) push(j, lane_on);
+            return;
+        }
+        // two kept beams per step: independent broadcasts and prefilters (ILP), then the survivors
+        // are queued beam by beam in order
+        unsigned long long todo = km;
+        while (todo != 0ull) {
+            const int j1 = __ffsll((long long)todo) - 1;
+            todo &= todo - 1ull;
+            const bool two = todo != 0ull;
+            const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
+            if (two) todo &= todo - 1ull;
+            const ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);  // both beams' reads issued together
+            const bool f1 = scan_far(SL, L.au, B1), f2 = scan_far(SL, L.au, B2);
+            const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
+            const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
+            push(j1, n1);
+            if (two) push(j2, n2);
         }
     };
 
     if (__ballot(valid) != 0ull) {
         const int32_t root = roots[sub];
+        // the production instantiation re-reads the lane's o, tmax and 1/d from its SegRec at each
+        // node visit instead of holding them in VGPRs through the leaf scans (register budget)
+        const float4 *my = reinterpret_cast<const float4 *>(srec + (s < nseg ? s : nseg - 1));
         if (root < 0) {
             leaf(root, valid);
         } else {
@@ -470,9 +537,21 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 const NodeV n = load_node(nodes, node);
                 if (COUNT) ++visits;
                 const int32_t c0 = n.c0, c1 = n.c1;
+                f3 lo = L.o, li = L.invs;
+                float lt = L.tmax;
+                if (!COUNT) {
+                    // an opaque copy of the address per visit: keeps the compiler from hoisting the
+                    // two loads out of the loop (and the 7 values back into registers)
+                    const float4 *mp = my;
+                    asm volatile("" : "+v"(mp));
+                    const float4 a0 = mp[0], a3 = mp[3];
+                    lo = mk(a0.x, a0.y, a0.z);
+                    lt = a0.w;
+                    li = mk(a3.x, a3.y, a3.z);
+                }
                 float te0 = 0.f, te1 = 0.f;
-                const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, L.o, L.invs, L.tmax, te0);
-                const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, L.o, L.invs, L.tmax, te1);
+                const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, lo, li, lt, te0);
+                const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, lo, li, lt, te1);
                 const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
                 bool go0 = m0 != 0ull, go1 = m1 != 0ull;
                 if (go0 && c0 < 0) {
@@ -517,7 +596,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         __builtin_amdgcn_wave_barrier();
         if (t1 > h1) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_box_exact(sh, L, h1, t1 - h1, recs, pw, R, sd, seg0, count_c);
+            tile_exact(sh, h1, t1 - h1, srec, sd, seg0, recs, pw, R, count_c);
         }
         h1 = t1 = 0;
     }
@@ -545,6 +624,22 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             atomicAdd(&ctr->ccp_wave_evals, pf.ccp_waves);
         }
     }
+}
+
+// One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec): the values
+// load_lane derives, computed once per gather instead of once per (packet, subtree) wave.
+__global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__restrict__ so,
+                                                  const float *__restrict__ sp_, const float *__restrict__ sd,
+                                                  const float *__restrict__ stmax, SegRec *__restrict__ out) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    Lane L;
+    load_lane(s, nseg, so, sp_, sd, stmax, L);
+    float4 *q = reinterpret_cast<float4 *>(out + s);
+    q[0] = make_float4(L.o.x, L.o.y, L.o.z, L.tmax);
+    q[1] = make_float4(L.p.x, L.p.y, L.p.z, L.mag_a);
+    q[2] = make_float4(L.au.x, L.au.y, L.au.z, __int_as_float(L.has_inf ? 1 : 0));
+    q[3] = make_float4(L.invs.x, L.invs.y, L.invs.z, L.omax);
 }
 
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the
@@ -749,11 +844,19 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     // per-subtree counts: candidates + contributions with counters, contributions alone otherwise
     int32_t *pcnt = (counters || a.seg_counts) ? a.pcnt : nullptr;
     if ((counters || a.seg_counts) && !pcnt) return hipErrorInvalidValue;
+    if (!a.segrec || a.leaf_size > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
+                       a.tmax, a.segrec);
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
-    hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax, a.R,  \
-                       a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots, a.split, a.ctr,   \
-                       stack_cap, (int)a.prefilter)
+    if (a.scan_mode == 1)                                                                                        \
+        hipLaunchKernelGGL((k_gather_tile<C, W, false>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d,   \
+                           a.tmax, a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size,   \
+                           a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter);                                 \
+    else                                                                                                         \
+    hipLaunchKernelGGL((k_gather_tile<C, W, true>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,       \
+                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
+                       a.split, a.ctr, stack_cap, (int)a.prefilter)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

@@ -50,6 +50,21 @@ class ShardedFrame:
     def npix(self) -> int:
         return self.w * self.h
 
+    def band(self):
+        """This rank's owned pixels packed into a contiguous (band_len, 3) band (zero padded)."""
+        import torch
+
+        band = torch.zeros((self.band_len, 3), dtype=torch.float32, device=self.device)
+        band[: self._idx.shape[0]] = self.accum.index_select(0, self._idx)
+        return band
+
+    def scatter_bands(self, parts, skip: int | None = None):
+        """Write every rank's band (parts[r]) back to its tiles of this frame (rank `skip` left as is)."""
+        for r, idx in enumerate(self._all_idx):
+            if r != skip:
+                self.accum.index_copy_(0, idx, parts[r][: idx.shape[0]].to(self.accum.device))
+        return self.accum
+
     def gather_to_root(self, root: int = 0):
         """One collective per written image: each rank's band of owned pixels (packed, 1/N of the
         film) is gathered to `root`, which scatters the bands into the full film.  Returns the full
@@ -59,14 +74,11 @@ class ShardedFrame:
 
         if self.world == 1:
             return self.accum
-        band = torch.zeros((self.band_len, 3), dtype=torch.float32, device=self.device)
-        band[: self._idx.shape[0]] = self.accum.index_select(0, self._idx)
+        band = self.band()
         parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None
         dist.gather(band, gather_list=parts, dst=root)
         if self.rank == root:
-            for r, idx in enumerate(self._all_idx):
-                if r != root:
-                    self.accum.index_copy_(0, idx, parts[r][: idx.shape[0]])
+            self.scatter_bands(parts, skip=root)
         return self.accum
 
     # the round-1 name (a reduce of full frames); kept as an alias of the gather

@@ -80,6 +80,7 @@ def parse(argv=None):
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--scan-mode", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -170,6 +171,8 @@ def main():
         g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
     if args.sort_key >= 0:
         g.set_option(105, args.sort_key)
+    if args.scan_mode >= 0:
+        g.set_option(106, args.scan_mode)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
@@ -528,6 +531,35 @@ class SyntheticWorkload:
                 "split": a.split, "prefilter": bool(a.prefilter)}
 
 
+def host_threads():
+    """The host threads this process may really use: its CPU affinity, capped by a cgroup CPU quota
+    (a GPU box's share of a large host: affinity can list every CPU of the machine while the quota
+    allows ~16), and by OMP_NUM_THREADS when that is set (the box sets it to its share)."""
+    n = len(os.sched_getaffinity(0))
+    notes = [f"affinity {n}"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(per)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    if quota:
+        notes.append(f"cgroup quota {quota}")
+        n = min(n, quota)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        notes.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, int(omp))
+    return n, ", ".join(notes)
+
+
 def cpu_baseline(wl, args, gather_per_step):
     """Oracle = CPU restatement of the reference algorithm (not pbrt itself: the reference build was
     denied).  For the first and the last timed iteration: the SAH build single-threaded
@@ -539,7 +571,7 @@ def cpu_baseline(wl, args, gather_per_step):
     from oracle_lib import load_oracle
 
     ora = load_oracle()
-    threads = len(os.sched_getaffinity(0))
+    threads, cpu_note = host_threads()
     iters = sorted({0, args.steps - 1}) if wl.name != "synthetic" else [0]
     per_it, visit, cand = [], [], []
     for it in iters:
@@ -565,8 +597,9 @@ def cpu_baseline(wl, args, gather_per_step):
         tgt = args.cpu_seconds / len(iters)
         m = int(min(n, max(8 * threads, tgt / per_seg)))
         g_s, out = timed(m, threads)
-        m1 = int(min(n - m, max(4, 0.25 * tgt / (per_seg * threads))))
-        g1_s, _ = timed(m1, 1, off=m)
+        dt1, _ = timed(2, 1, off=m)
+        m1 = int(min(n - m - 2, max(4, 0.5 * tgt / max(dt1 / 2, 1e-3))))
+        g1_s, _ = timed(m1, 1, off=m + 2)
         bvh.close()
         nb = beams["radius"].shape[0]
         rec = {"iteration": it, "beams": nb, "sah_build_s": build_s, "segments_all_threads": m,
@@ -587,10 +620,11 @@ def cpu_baseline(wl, args, gather_per_step):
             "nproc": os.cpu_count(),
             "kind": "port",
             "value_1_thread": value1,
+            "threads_note": cpu_note,
             "sample": (f"random camera segments of the {wl.name} workload at iterations {iters} (the first and last "
                        f"timed iterations), gathered against all of that iteration's beams through the oracle's SAH "
-                       f"tree: {threads} threads (every CPU this process may use; nproc {os.cpu_count()}) and 1 thread; "
-                       f"value = 1 / mean seconds per estimate over those iterations"),
+                       f"tree: {threads} threads (every CPU this process may use: {cpu_note}; nproc {os.cpu_count()}) "
+                       f"and 1 thread; value = 1 / mean seconds per estimate over those iterations"),
             "per_iteration": per_it,
         },
         "visit_mean": float(np.mean(visit)),

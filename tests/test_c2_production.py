@@ -6,8 +6,8 @@ coherence sort and gather run exactly as bench.py times them (kernel 0, counters
 on); bre_gather_camera_segments only scatters the per-segment sums and the contribution counts
 (counted by the production instantiation's own control flow) back to camera-pass order.  ~1,000
 randomly sampled segments are then gathered by the oracle (reference SAH tree over the FULL beam
-set, photonbeam.cpp:494-508) and compared: contribution counts exactly, per-segment RGB within
-1e-5 relative (summation order only).  The pixel sums are also checked against the per-segment
+set, photonbeam.cpp:494-508) and compared: contribution counts exactly, per-segment RGB within the
+float32 summation-order bound max(1e-5, 4 u sqrt(n)) relative (n contributions, u = 2^-24).  The pixel sums are also checked against the per-segment
 sums (the scatter and the production accumulation agree)."""
 import numpy as np
 import pytest
@@ -53,6 +53,11 @@ def test_c2_production_gather_matches_oracle_per_segment(bre, oracle, scene_mod_
     bvh.close()
     assert ref["contrib"].sum() > 1_000_000  # dense real data (~49k contributions per segment at C2)
     assert np.array_equal(counts[idx, 1], ref["contrib"]), "production contribution counts differ"
-    scale = np.maximum(np.abs(ref["seg_rgb"]).max(axis=1, keepdims=True), 1e-30)
-    err = float((np.abs(seg_rgb[idx] - ref["seg_rgb"]) / scale).max())
-    assert err <= 1e-5, err
+    # per-segment tolerance: both sides are float32 sums of the same n positive terms in different
+    # orders; each sum's rounding error has a std of ~u sqrt(n) / 3 relative (u = 2^-24), so the
+    # difference is held to 4 u sqrt(n) (~8.5 sigma; 5.3e-5 at C2's ~49k terms), floor 1e-5
+    scale = np.maximum(np.abs(ref["seg_rgb"]).max(axis=1), 1e-30)
+    err = np.abs(seg_rgb[idx] - ref["seg_rgb"]).max(axis=1) / scale
+    tol = np.maximum(1e-5, 4 * 2.0 ** -24 * np.sqrt(ref["contrib"].astype(np.float64)))
+    worst = int(np.argmax(err / tol))
+    assert (err <= tol).all(), (float(err[worst]), float(tol[worst]), int(ref["contrib"][worst]))

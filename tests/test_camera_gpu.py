@@ -5,8 +5,9 @@ Bars:
 * camera segments: BIT-EXACT, compared as sets keyed by (pixel, depth) since the GPU emits them
   depth-major in 8x8-tile order and the oracle pixel by pixel;
 * surface radiance (rendersurfaces): BIT-EXACT per pixel (same operations in the same order);
-* full iteration / full render image (gather + surface terms): relative L2 <= 1e-3 (north star;
-  float summation order of the gather differs), exact candidate-free pixels agree.
+* full iteration / full render image (gather + surface terms): relative L2 <= 1e-5 and every pixel
+  within 1e-4 of its own magnitude where it is not tiny (the photon and camera passes are bit-exact,
+  only the float summation order of the gather differs; the north star allows 1e-3).
 """
 import importlib
 
@@ -117,6 +118,18 @@ def _rel_l2(a, b):
     return float(np.linalg.norm(a.astype(np.float64) - b) / max(np.linalg.norm(b), 1e-300))
 
 
+def _assert_image_close(got, ref, l2=1e-5, px=1e-4):
+    """Relative L2 over the image, plus a per-pixel bound: a pixel whose largest channel is above
+    1e-3 of the image maximum must agree to `px` of that channel (dropped or doubled contributions
+    show up here even when the image L2 hides them)."""
+    got, ref = got.reshape(-1, 3).astype(np.float64), ref.reshape(-1, 3).astype(np.float64)
+    assert _rel_l2(got, ref) <= l2, _rel_l2(got, ref)
+    mag = np.abs(ref).max(axis=1)
+    big = mag > 1e-3 * mag.max()
+    err = np.abs(got - ref).max(axis=1)
+    assert (err[big] <= px * mag[big]).all(), float((err[big] / mag[big]).max())
+
+
 def test_render_iteration_matches_oracle(bre, oracle, scene_mod, torch):
     s = scene_mod.cornell_scene()
     w, h, photons, depth = 64, 48, 20000, 5
@@ -128,7 +141,7 @@ def test_render_iteration_matches_oracle(bre, oracle, scene_mod, torch):
     R2 = bre.beam_radius_at(0.05, 0.5, 2)
     ref = _oracle_iteration(oracle, s, w, h, 2, photons, depth, R2)
     got = ld.cpu().numpy()
-    assert _rel_l2(got, ref) <= 1e-3
+    _assert_image_close(got, ref)
     assert got.mean() > 0
 
 
@@ -147,7 +160,7 @@ def test_render_matches_iterations(bre, oracle, scene_mod, torch):
                                  rs=False)
     ref /= 3
     assert img.shape == (h, w, 3)
-    assert _rel_l2(img.reshape(-1, 3), ref) <= 1e-3
+    _assert_image_close(img, ref)
     del R
 
 
@@ -224,8 +237,30 @@ def test_render_iteration_grid_matches_oracle(bre, oracle, scene_mod, torch):
     R1 = bre.beam_radius_at(0.03, 0.5, 1)
     ref = _oracle_iteration(oracle, s, w, h, 1, photons, depth, R1)
     got = ld.cpu().numpy()
-    assert _rel_l2(got, ref) <= 1e-3
+    _assert_image_close(got, ref)
     assert got.mean() > 0
+
+
+@pytest.mark.parametrize("start", [0, 4])
+def test_progressive_grid_render_c5_style(bre, oracle, scene_mod, torch, start):
+    """C5 in small (BASELINE configs[4]): 10 progressive shrinking-radius passes on the
+    heterogeneous smoke (GridDensityMedium, HG g 0.7), R_{i+1} = R_i (i + alpha) / (i + 1)
+    (photonbeam.cpp:354-356, 562), image = Ld / end_iteration (:565-583).  With start_iteration 4 the
+    radius catches up over the skipped passes (:354-356) and the image still divides by 10 (:578)."""
+    s = scene_mod.cornell_smoke_scene(n=32)
+    w, h, photons, depth, n_it = 40, 32, 8000, 5, 10
+    p = scene_mod.render_params(w, h, iterations=n_it, photons=photons, max_depth=depth, radius=0.05, alpha=0.5,
+                                start_iteration=start)
+    with bre.BeamGather(0) as g:
+        img = g.render(s, p)
+    ref = np.zeros((w * h, 3))
+    for it in range(start, n_it):
+        R = np.float32(bre.beam_radius_at(0.05, 0.5, it))
+        assert R == np.float32(oracle.radius_at(0.05, 0.5, it))
+        ref += _oracle_iteration(oracle, s, w, h, it, photons, depth, R)
+    ref /= n_it
+    _assert_image_close(img, ref)
+    assert img.mean() > 0
 
 
 def test_segment_sort_changes_no_pixel(bre, scene_mod, torch):

@@ -1,0 +1,56 @@
+"""libbre under image-tile sharding (dist.py), on one GPU: the film's 16x16 tiles
+(photonbeam.cpp:344-347) are rendered as N shards one after another through the C ABI
+(BRE_OPT_SHARD_RANK / BRE_OPT_SHARD_COUNT, exactly what each rank of bench.py --gpus N does), the
+shards' owned-pixel bands are packed and scattered back by dist.ShardedFrame (the payload of the RCCL
+gather), and the assembled film must equal the 1-shard render: every pixel is summed from the same
+segments' contributions (float summation order of the pixel atomics aside)."""
+import importlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_l2(a, b):
+    a, b = a.astype(np.float64), b.astype(np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.mark.parametrize("world,shape,photons", [(4, (256, 192), 200_000), (8, (512, 512), 300_000)])
+def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, photons):
+    import torch
+
+    dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
+    W, H = shape
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+    it, R = 3, bre.beam_radius_at(0.01, 0.5, 3)
+
+    def render(rank, count, frame):
+        with bre.BeamGather(0) as g:
+            g.set_shard(rank, count)
+            g.trace_photons(scene, photons, it, 5, R)
+            n = g.camera_pass(scene, W, H, it, 5, True, True, surface=frame.accum)
+            g.gather_camera(R, frame.accum)
+            g.synchronize()
+        return n
+
+    ref = dmod.ShardedFrame(W, H, 0, 1, device="cuda")
+    n_ref = render(0, 1, ref)
+    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda") for r in range(world)]
+    n_sh = sum(render(r, world, f) for r, f in enumerate(frames))
+    assert n_sh == n_ref  # the shards partition the camera segments
+    owned = np.zeros(W * H, bool)
+    for f in frames:
+        acc = f.accum.cpu().numpy()
+        outside = np.ones(W * H, bool)
+        outside[f.pixels] = False
+        assert not acc[outside].any()  # a rank writes only its own tiles
+        owned[f.pixels] = True
+    assert owned.all()
+    root = frames[0]
+    root.scatter_bands([f.band() for f in frames], skip=0)  # what gather_to_root does over RCCL
+    got, want = root.accum.cpu().numpy(), ref.accum.cpu().numpy()
+    assert _rel_l2(got, want) <= 1e-6
+    big = want.max(axis=1) > 1e-3 * want.max()
+    assert (np.abs(got - want)[big] <= 1e-4 * np.abs(want[big]).max(axis=1, keepdims=True)).all()
