@@ -673,6 +673,17 @@ static bre_status check_medium(bre_ctx *c, const bre_scene *scene, const char *f
     return BRE_OK;
 }
 
+// Triangle count in range and at least one area light (the passes need scene.lights non-empty)
+static bre_status check_scene(bre_ctx *c, const bre_scene *scene, const char *fn) {
+    if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "%s: null scene", fn);
+    if (scene->n_triangles < 1 || scene->n_triangles > BRE_MAX_TRIANGLES)
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: triangle count must be in 1..%d", fn, BRE_MAX_TRIANGLES);
+    int lights = 0;
+    for (int i = 0; i < scene->n_triangles; ++i) lights += scene->triangles[i].emit != 0;
+    if (lights == 0) return fail(c, BRE_ERR_INVALID_ARG, "%s: the scene has no area light", fn);
+    return BRE_OK;
+}
+
 // DevScene (+ the density grid of a GridDensityMedium) into ph_scene on the context's stream
 static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
     const float *dd = nullptr;
@@ -700,10 +711,9 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     if (n_photons < 0 || iteration < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: negative count");
     if (max_depth < 1 || max_depth > BRE_MAX_DEPTH)
         return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: max_depth must be in [1, %d]", BRE_MAX_DEPTH);
-    if (scene->n_quads < 1 || scene->n_quads > BRE_MAX_QUADS || scene->light_quad < 0 ||
-        scene->light_quad >= scene->n_quads)
-        return fail(c, BRE_ERR_INVALID_ARG, "bre_trace_photons: bad quad count or light index");
-    bre_status st = check_medium(c, scene, "bre_trace_photons");
+    bre_status st = check_scene(c, scene, "bre_trace_photons");
+    if (st != BRE_OK) return st;
+    st = check_medium(c, scene, "bre_trace_photons");
     if (st != BRE_OK) return st;
     st = set_device(c);
     if (st != BRE_OK) return st;
@@ -774,13 +784,7 @@ bre_status bre_get_beams(bre_ctx *c, int64_t capacity, float *start, float *end,
     return check_flags(c);
 }
 
-static bre_status check_scene(bre_ctx *c, const bre_scene *scene, const char *fn) {
-    if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "%s: null scene", fn);
-    if (scene->n_quads < 1 || scene->n_quads > BRE_MAX_QUADS || scene->light_quad < 0 ||
-        scene->light_quad >= scene->n_quads)
-        return fail(c, BRE_ERR_INVALID_ARG, "%s: bad quad count or light index", fn);
-    return BRE_OK;
-}
+
 
 bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, int32_t height, int32_t iteration,
                            int32_t max_depth, int32_t render_surfaces, int32_t render_media, float *d_surface,
@@ -1036,30 +1040,33 @@ bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_param
 void bre_scene_cornell(bre_scene *s, float sigma_a, float sigma_s, float g) {
     if (!s) return;
     memset(s, 0, sizeof(*s));
-    struct Q {
-        float p0[3], e1[3], e2[3], kd[3];
+    // scenes/cornell_world.pbrt: one "trianglemesh" per wall, indices [0 1 2 0 2 3]
+    struct M {
+        float v[4][3], kd[3];
+        int emit;
     };
     const float W = 0.73f, R0 = 0.63f, R1 = 0.065f, R2 = 0.05f, G0 = 0.14f, G1 = 0.45f, G2 = 0.091f;
-    const Q qs[7] = {
-        {{0, 0, 0}, {0, 0, 1}, {1, 0, 0}, {W, W, W}},          // floor, normal +y
-        {{0, 1, 0}, {1, 0, 0}, {0, 0, 1}, {W, W, W}},          // ceiling, normal -y
-        {{0, 0, 1}, {0, 1, 0}, {1, 0, 0}, {W, W, W}},          // back wall, normal -z
-        {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {W, W, W}},          // front wall (behind camera), normal +z
-        {{0, 0, 0}, {0, 1, 0}, {0, 0, 1}, {R0, R1, R2}},       // left wall (red), normal +x
-        {{1, 0, 0}, {0, 0, 1}, {0, 1, 0}, {G0, G1, G2}},       // right wall (green), normal -x
-        {{0.35f, 0.999f, 0.35f}, {0.3f, 0, 0}, {0, 0, 0.3f}, {0, 0, 0}},  // light, normal -y
+    const M ms[7] = {
+        {{{0, 0, 0}, {0, 0, 1}, {1, 0, 1}, {1, 0, 0}}, {W, W, W}, 0},          // floor, normal +y
+        {{{0, 1, 0}, {1, 1, 0}, {1, 1, 1}, {0, 1, 1}}, {W, W, W}, 0},          // ceiling, normal -y
+        {{{0, 0, 1}, {0, 1, 1}, {1, 1, 1}, {1, 0, 1}}, {W, W, W}, 0},          // back wall, normal -z
+        {{{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}}, {W, W, W}, 0},          // front wall (behind camera), +z
+        {{{0, 0, 0}, {0, 1, 0}, {0, 1, 1}, {0, 0, 1}}, {R0, R1, R2}, 0},       // left wall (red), +x
+        {{{1, 0, 0}, {1, 0, 1}, {1, 1, 1}, {1, 1, 0}}, {G0, G1, G2}, 0},       // right wall (green), -x
+        {{{0.35f, 0.999f, 0.35f}, {0.65f, 0.999f, 0.35f}, {0.65f, 0.999f, 0.65f}, {0.35f, 0.999f, 0.65f}},
+         {0, 0, 0}, 1},                                                         // light, normal -y
     };
-    s->n_quads = 7;
-    for (int i = 0; i < 7; ++i) {
-        memcpy(s->quads[i].p0, qs[i].p0, 12);
-        memcpy(s->quads[i].e1, qs[i].e1, 12);
-        memcpy(s->quads[i].e2, qs[i].e2, 12);
-        memcpy(s->quads[i].kd, qs[i].kd, 12);
-    }
-    s->light_quad = 6;
-    s->light_L[0] = 17.f;
-    s->light_L[1] = 12.f;
-    s->light_L[2] = 4.f;
+    const float Le[3] = {17.f, 12.f, 4.f};
+    const int idx[6] = {0, 1, 2, 0, 2, 3};
+    s->n_triangles = 14;
+    for (int m = 0; m < 7; ++m)
+        for (int t = 0; t < 2; ++t) {
+            bre_triangle &T = s->triangles[2 * m + t];
+            for (int v = 0; v < 3; ++v) memcpy(T.p[v], ms[m].v[idx[3 * t + v]], 12);
+            memcpy(T.kd, ms[m].kd, 12);
+            T.emit = ms[m].emit;
+            if (T.emit) memcpy(T.Le, Le, 12);
+        }
     s->has_medium = 1;
     for (int k = 0; k < 3; ++k) {
         s->sigma_a[k] = sigma_a;

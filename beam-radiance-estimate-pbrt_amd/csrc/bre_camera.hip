@@ -260,13 +260,13 @@ __device__ __forceinline__ int64_t halton_index(const DevCamera &C, int px, int 
     return off + sample_num * C.stride;
 }
 
-// ---- matte quad BSDF (reflection.cpp:650-768) ----
-__device__ __forceinline__ f3 to_local(const PQuad &q, f3 v) { return mk(dot3(v, q.ss), dot3(v, q.ts), dot3(v, q.n)); }
-__device__ __forceinline__ f3 to_world(const PQuad &q, f3 v) {
+// ---- matte triangle BSDF (reflection.cpp:650-768) ----
+__device__ __forceinline__ f3 to_local(const PTri &q, f3 v) { return mk(dot3(v, q.ss), dot3(v, q.ts), dot3(v, q.n)); }
+__device__ __forceinline__ f3 to_world(const PTri &q, f3 v) {
     return mk(q.ss.x * v.x + q.ts.x * v.y + q.n.x * v.z, q.ss.y * v.x + q.ts.y * v.y + q.n.y * v.z,
               q.ss.z * v.x + q.ts.z * v.y + q.n.z * v.z);
 }
-__device__ __forceinline__ void bsdf_f(const PQuad &q, f3 wo_w, f3 wi_w, float f[3]) {
+__device__ __forceinline__ void bsdf_f(const PTri &q, f3 wo_w, f3 wi_w, float f[3]) {
     f[0] = f[1] = f[2] = 0.f;
     if (q.absorb) return;
     if (to_local(q, wo_w).z == 0) return;
@@ -274,7 +274,7 @@ __device__ __forceinline__ void bsdf_f(const PQuad &q, f3 wo_w, f3 wi_w, float f
     if (reflect)
         for (int c = 0; c < 3; ++c) f[c] = 0.f + q.kd[c] * kInvPi;
 }
-__device__ __forceinline__ float bsdf_pdf(const PQuad &q, f3 wo_w, f3 wi_w) {
+__device__ __forceinline__ float bsdf_pdf(const PTri &q, f3 wo_w, f3 wi_w) {
     if (q.absorb) return 0.f;
     const f3 wo = to_local(q, wo_w), wi = to_local(q, wi_w);
     if (wo.z == 0) return 0.f;
@@ -283,7 +283,7 @@ __device__ __forceinline__ float bsdf_pdf(const PQuad &q, f3 wo_w, f3 wi_w) {
     return pdf / 1;
 }
 // BSDF::Sample_f; *pdf untouched when wo.z == 0 (as the reference); returns false for f = 0
-__device__ __forceinline__ bool bsdf_sample(const PQuad &q, f3 wo_w, float ux, float uy, f3 &wi_w, float &pdf,
+__device__ __forceinline__ bool bsdf_sample(const PTri &q, f3 wo_w, float ux, float uy, f3 &wi_w, float &pdf,
                                             float f[3]) {
     f[0] = f[1] = f[2] = 0.f;
     if (q.absorb) {
@@ -306,23 +306,22 @@ __device__ __forceinline__ float power_heuristic(float fpdf, float gpdf) {
     return (f * f) / (f * f + g * g);
 }
 
-// EstimateDirect for the scene's one area light (integrator.cpp:108-214), handleMedia = true
-__device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr, const PQuad &q, f3 wo, float usx,
-                                float usy, float ulx, float uly, float Ld[3]) {
-    const PQuad &L = S.q[S.light];
+// EstimateDirect (integrator.cpp:108-214) for the area light on triangle `li`, handleMedia = true
+__device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr, const PTri &q, f3 wo, int li,
+                                float usx, float usy, float ulx, float uly, float Ld[3]) {
+    const PTri &L = S.t[li];
     Ld[0] = Ld[1] = Ld[2] = 0.f;
     float scat_pdf = 0.f;
-    // DiffuseAreaLight::Sample_Li -> Shape::Sample(ref, u)
-    const f3 ue1 = scale3(L.e1, ulx), ve2 = scale3(L.e2, uly);
-    const f3 sp = add3(add3(L.p0, ue1), ve2);
-    const f3 sperr = scale3(add3(add3(abs3(L.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
-    float light_pdf = 1 / L.area;
+    // DiffuseAreaLight::Sample_Li (diffuse.cpp:68-81) -> Shape::Sample(ref, u) (shape.cpp:56-70)
+    const ShapeSample ps = sample_tri(L, ulx, uly);
+    const f3 sp = ps.p;
+    float light_pdf = ps.pdf;
     f3 w = sub3(sp, p);
     if (lensq3(w) == 0) {
         light_pdf = 0;
     } else {
         w = normalize3(w);
-        light_pdf *= lensq3(sub3(p, sp)) / fabsf(dot3(L.n, neg3(w)));
+        light_pdf *= lensq3(sub3(p, sp)) / fabsf(dot3(ps.n, neg3(w)));
         if (isinf(light_pdf)) light_pdf = 0.f;
     }
     f3 wi = mk(0, 0, 0);
@@ -331,8 +330,8 @@ __device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr,
         light_pdf = 0;
     } else {
         wi = normalize3(sub3(sp, p));
-        if (dot3(L.n, neg3(wi)) > 0)
-            for (int c = 0; c < 3; ++c) Li[c] = S.Le[c];
+        if (dot3(ps.n, neg3(wi)) > 0)
+            for (int c = 0; c < 3; ++c) Li[c] = L.Le[c];
     }
     if (light_pdf > 0 && !black3(Li)) {
         float f[3];
@@ -343,12 +342,12 @@ __device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr,
         if (!black3(f)) {
             // VisibilityTester::Tr over Interaction::SpawnRayTo(pShape)
             const f3 ro = offset_origin(p, perr, q.n, sub3(sp, p));
-            const f3 target = offset_origin(sp, sperr, L.n, sub3(ro, sp));
+            const f3 target = offset_origin(sp, ps.perr, ps.n, sub3(ro, sp));
             const f3 rd = sub3(target, ro);
             float tmax = 1 - 0.0001f;
             Hit h;
             if (intersect_scene(S, ro, rd, tmax, h)) {
-                Li[0] = Li[1] = Li[2] = 0.f;  // every quad has a material
+                Li[0] = Li[1] = Li[2] = 0.f;  // every triangle has a material
             } else if (S.medium) {
                 float tr[3];
                 medium_tr_any(S, hs, ro, rd, tmax, tr);
@@ -367,10 +366,11 @@ __device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr,
         const float ad = fabsf(dot3(wi, q.n));
         for (int c = 0; c < 3; ++c) f[c] = f[c] * ad;
         if (!black3(f) && scat_pdf > 0) {
+            // DiffuseAreaLight::Pdf_Li -> Shape::Pdf(ref, wi) (shape.cpp:72-87): this triangle alone
             const f3 ro = offset_origin(p, perr, q.n, wi);
             float tl;
             Hit hl;
-            if (!intersect_quad(L, ro, wi, __builtin_huge_valf(), tl, hl)) return;
+            if (!intersect_tri(L, ro, wi, __builtin_huge_valf(), tl, hl)) return;
             light_pdf = lensq3(sub3(p, hl.p)) / (fabsf(dot3(L.n, neg3(wi))) * L.area);
             if (isinf(light_pdf)) light_pdf = 0.f;
             if (light_pdf == 0) return;
@@ -384,8 +384,9 @@ __device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr,
                 medium_tr_any(S, hs, ro, wi, tmax, t2);
                 for (int c = 0; c < 3; ++c) tr[c] = tr[c] * t2[c];
             }
-            if (found && h.quad == S.light && dot3(L.n, neg3(wi)) > 0 && !black3(S.Le))
-                for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + f[c] * S.Le[c] * tr[c] * wgt / scat_pdf;
+            // lightIsect.primitive->GetAreaLight() == &light: the same triangle, one-sided
+            if (found && h.tri == li && dot3(L.n, neg3(wi)) > 0 && !black3(L.Le))
+                for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + f[c] * L.Le[c] * tr[c] * wgt / scat_pdf;
         }
     }
 }
@@ -459,18 +460,20 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
         }
         for (int c = 0; c < 3; ++c) beta[c] = beta[c] * mb[c];
         if (!render_surfaces) break;
-        const PQuad &q = S.q[hit.quad];
+        const PTri &q = S.t[hit.tri];
         const f3 wo = neg3(d);
-        if (depth == 0 && hit.quad == S.light && dot3(q.n, wo) > 0)
-            for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + beta[c] * S.Le[c];
-        // UniformSampleOneLight: light choice, uLight, uScattering (integrator.cpp:85-106)
-        (void)hs.get1d();
+        // isect.Le(wo): the triangle's own area light, one-sided (diffuse.h:56-58)
+        if (depth == 0 && q.emit && dot3(q.n, wo) > 0)
+            for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + beta[c] * q.Le[c];
+        // UniformSampleOneLight (integrator.cpp:54-82): light uniformly, uLight, uScattering
+        const int ln = min((int)(hs.get1d() * S.n_lights), S.n_lights - 1);
+        const float light_pdf = 1.f / (float)S.n_lights;  // Float(1) / nLights
         float ulx, uly, usx, usy;
         hs.get2d(ulx, uly);
         hs.get2d(usx, usy);
         float ed[3];
-        estimate_direct(S, hs, hit.p, hit.perr, q, normalize3(wo), usx, usy, ulx, uly, ed);
-        for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + beta[c] * (ed[c] / 1.0f);
+        estimate_direct(S, hs, hit.p, hit.perr, q, normalize3(wo), S.light_tri[ln], usx, usy, ulx, uly, ed);
+        for (int c = 0; c < 3; ++c) Ld[c] = Ld[c] + beta[c] * (ed[c] / light_pdf);
         if (depth < max_depth - 1) {
             float ux, uy, pdf = 0.f, f[3];
             hs.get2d(ux, uy);

@@ -33,8 +33,7 @@ float grid_max_density(const bre_scene *s) {
 
 void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
     DevScene d{};
-    d.n_quads = s->n_quads;
-    d.light = s->light_quad;
+    d.n_tris = s->n_triangles;
     d.medium = s->has_medium == BRE_MEDIUM_GRID ? BRE_MEDIUM_GRID : (s->has_medium ? BRE_MEDIUM_HOMOGENEOUS : 0);
     if (d.medium == BRE_MEDIUM_GRID) {
         // GridDensityMedium ctor (grid.h:58-77): sigma_t = (sigma_a + sigma_s)[0]; invMaxDensity
@@ -44,26 +43,53 @@ void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
         for (int k = 0; k < 16; ++k) d.w2m[k] = s->world_to_medium[k];
         d.density = d_density;
     }
-    for (int c = 0; c < 3; ++c) {
-        d.Le[c] = s->light_L[c];
+    for (int c = 0; c < 3; ++c)
         d.sigma_t[c] = s->sigma_a[c] + s->sigma_s[c];  // HomogeneousMedium ctor: sigma_a + sigma_s
-    }
     d.g = s->g;
-    for (int i = 0; i < s->n_quads; ++i) {
-        const bre_quad &q = s->quads[i];
-        PQuad &Q = d.q[i];
-        Q.p0 = mk(q.p0[0], q.p0[1], q.p0[2]);
-        Q.e1 = mk(q.e1[0], q.e1[1], q.e1[2]);
-        Q.e2 = mk(q.e2[0], q.e2[1], q.e2[2]);
-        const f3 c = cross3d(Q.e1, Q.e2);
-        Q.area = len3(c);
-        Q.n = normalize3(c);
-        Q.ss = normalize3(Q.e1);
-        Q.ts = cross3d(Q.n, Q.ss);
-        Q.inv_e1sq = 1 / dot3(Q.e1, Q.e1);
-        Q.inv_e2sq = 1 / dot3(Q.e2, Q.e2);
-        for (int k = 0; k < 3; ++k) Q.kd[k] = q.kd[k];
-        Q.absorb = (q.kd[0] == 0 && q.kd[1] == 0 && q.kd[2] == 0) ? 1 : 0;
+    int nl = 0;
+    for (int i = 0; i < s->n_triangles; ++i) {
+        const bre_triangle &t = s->triangles[i];
+        PTri &T = d.t[i];
+        T.p0 = mk(t.p[0][0], t.p[0][1], t.p[0][2]);
+        T.p1 = mk(t.p[1][0], t.p[1][1], t.p[1][2]);
+        T.p2 = mk(t.p[2][0], t.p[2][1], t.p[2][2]);
+        const f3 dp02 = sub3(T.p0, T.p2), dp12 = sub3(T.p1, T.p2);
+        // dpdu for pbrt's default uvs (0,0), (1,0), (1,1): (duv12[1] dp02 - duv02[1] dp12) invdet
+        // with duv12[1] = duv02[1] = -1, invdet = 1 (triangle.cpp:276-285)
+        const f3 dpdu = scale3(sub3(scale3(dp02, -1.f), scale3(dp12, -1.f)), 1.f);
+        T.n = normalize3(cross3d(dp02, dp12));
+        T.ns = normalize3(cross3d(sub3(T.p1, T.p0), sub3(T.p2, T.p0)));
+        if (t.flip) {
+            T.n = neg3(T.n);
+            T.ns = neg3(T.ns);
+        }
+        T.ss = normalize3(dpdu);
+        T.ts = cross3d(T.n, T.ss);
+        T.area = (float)(0.5 * (double)len3(cross3d(sub3(T.p1, T.p0), sub3(T.p2, T.p0))));
+        for (int k = 0; k < 3; ++k) {
+            T.kd[k] = t.kd[k];
+            T.Le[k] = t.Le[k];
+        }
+        T.absorb = (t.kd[0] == 0 && t.kd[1] == 0 && t.kd[2] == 0) ? 1 : 0;
+        T.emit = t.emit != 0;
+        if (T.emit) {
+            d.light_tri[nl] = i;
+            // DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:64-66), .y()
+            float pw[3];
+            for (int k = 0; k < 3; ++k) pw[k] = ((T.Le[k] * 1.f) * T.area) * kPi;
+            d.light_func[nl] = lum3(pw);
+            ++nl;
+        }
+    }
+    d.n_lights = nl;
+    // Distribution1D(func, n) (sampling.h:57-69)
+    d.light_cdf[0] = 0;
+    for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] = d.light_cdf[i - 1] + d.light_func[i - 1] / (float)nl;
+    d.light_func_int = d.light_cdf[nl];
+    if (d.light_func_int == 0) {
+        for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] = (float)i / (float)nl;
+    } else {
+        for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] /= d.light_func_int;
     }
     *out = d;
 }
@@ -77,7 +103,7 @@ struct Frame {
     f3 o, d;     // photonRay
     float tmax;  // its surface hit distance
     f3 p, perr;  // isect.p and its error bound
-    int quad;
+    int tri;
     int depth;
     float beta[3];
 };
@@ -96,30 +122,29 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
     int64_t w = EMIT ? offsets[i] : 0;
     int cnt = 0;
 
-    // ---- emission, photonbeam.cpp:393-418 (one light: lightPdf = 1) ----
-    (void)pcg_float(rng);  // lightSample
+    // ---- emission, photonbeam.cpp:393-418: a light by power, DiffuseAreaLight::Sample_Le ----
+    float light_pdf;
+    const int ln = sample_light(S, pcg_float(rng), light_pdf);  // lightSample
     float u0x, u0y, u1x, u1y;
     pcg_2d(rng, u0x, u0y);
     pcg_2d(rng, u1x, u1y);
     (void)pcg_float(rng);  // uLightTime
-    const PQuad &L = S.q[S.light];
-    const f3 ue1 = scale3(L.e1, u0x), ve2 = scale3(L.e2, u0y);
-    const f3 lp = add3(add3(L.p0, ue1), ve2);
-    const f3 lperr = scale3(add3(add3(abs3(L.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
-    const float pdf_pos = 1 / L.area;
+    const PTri &L = S.t[S.light_tri[ln]];
+    const ShapeSample ps = sample_tri(L, u0x, u0y);
+    const float pdf_pos = ps.pdf;
     const f3 wl = cosine_hemisphere(u1x, u1y);
     const float pdf_dir = wl.z * kInvPi;
     f3 v1, v2;
-    coord_system(L.n, v1, v2);
-    f3 d = add3(add3(scale3(v1, wl.x), scale3(v2, wl.y)), scale3(L.n, wl.z));
-    f3 o = offset_origin(lp, lperr, L.n, d);
-    const bool front = dot3(L.n, d) > 0;  // DiffuseAreaLight::L, one-sided
+    coord_system(ps.n, v1, v2);
+    f3 d = add3(add3(scale3(v1, wl.x), scale3(v2, wl.y)), scale3(ps.n, wl.z));
+    f3 o = offset_origin(ps.p, ps.perr, ps.n, d);
+    const bool front = dot3(ps.n, d) > 0;  // DiffuseAreaLight::L, one-sided
     float beta[3];
-    bool alive = !(pdf_pos == 0 || pdf_dir == 0 || !front || black3(S.Le));
+    bool alive = !(pdf_pos == 0 || pdf_dir == 0 || !front || black3(L.Le));
     if (alive) {
-        const float ad = fabsf(dot3(L.n, d));
-        const float den = 1.0f * pdf_pos * pdf_dir;
-        for (int c = 0; c < 3; ++c) beta[c] = (ad * S.Le[c]) / den;
+        const float ad = fabsf(dot3(ps.n, d));
+        const float den = light_pdf * pdf_pos * pdf_dir;
+        for (int c = 0; c < 3; ++c) beta[c] = (ad * L.Le[c]) / den;
         alive = !black3(beta);
     }
 
@@ -156,7 +181,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
                     f.tmax = tmax;
                     f.p = hit.p;
                     f.perr = hit.perr;
-                    f.quad = hit.quad;
+                    f.tri = hit.tri;
                     f.depth = depth;
                     for (int c = 0; c < 3; ++c) {
                         f.beta[c] = beta[c];
@@ -189,7 +214,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
             // surface scattering (:296-323): Lambertian BSDF::Sample_f
             float ux, uy;
             pcg_2d(rng, ux, uy);
-            const PQuad &q = S.q[hit.quad];
+            const PTri &q = S.t[hit.tri];
             if (q.absorb) {
                 stop = true;
             } else {
@@ -234,7 +259,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
         tmax = f.tmax;
         hit.p = f.p;
         hit.perr = f.perr;
-        hit.quad = f.quad;
+        hit.tri = f.tri;
         depth = f.depth;
         for (int c = 0; c < 3; ++c) beta[c] = f.beta[c];
         resume = true;

@@ -141,21 +141,29 @@ BRE_TD f3 hg_sample(float g, f3 wo, float u0, float u1) {
     return add3(add3(scale3(v1, sin_t * cp), scale3(v2, sin_t * sp)), scale3(neg3(wo), cos_t));
 }
 
-// ---- scene on the device ----
-struct PQuad {
-    f3 p0, e1, e2, n, ss, ts;
-    float kd[3];
-    float inv_e1sq, inv_e2sq, area;
+// ---- scene on the device: pbrt Triangles (include/bre_scene.h) ----
+struct PTri {
+    f3 p0, p1, p2;
+    f3 n;        // Triangle::Intersect's normal: normalize(cross(p0 - p2, p1 - p2)), negated if flip
+    f3 ss, ts;   // BSDF frame: ss = normalize(dpdu), ts = cross(ns, ss)
+    f3 ns;       // Triangle::Sample's normal: normalize(cross(p1 - p0, p2 - p0)), negated if flip
+    float kd[3], Le[3];
+    float area;  // 0.5 * |cross(p1 - p0, p2 - p0)|
     int absorb;  // kd all zero: no BxDF
-    int pad;
+    int emit;    // a DiffuseAreaLight
 };
 
 struct DevScene {
-    int n_quads, light, medium, pad;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
-    float Le[3];
+    int n_tris, n_lights, medium, pad;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
     float sigma_t[3];
     float g;
-    PQuad q[BRE_MAX_QUADS];
+    // scene.lights (the emitting triangles, in order) and the Distribution1D of their Power().y()
+    // (ComputeLightPowerDistribution, integrator.cpp:217-225; sampling.h:55-69)
+    int light_tri[BRE_MAX_TRIANGLES];
+    float light_func[BRE_MAX_TRIANGLES];
+    float light_cdf[BRE_MAX_TRIANGLES + 1];
+    float light_func_int;
+    PTri t[BRE_MAX_TRIANGLES];
     // GridDensityMedium (grid.h:50-80): sigma_t = (sigma_a + sigma_s)[0], invMaxDensity
     int gn[3];
     float grid_sigma_t, grid_inv_max;
@@ -163,48 +171,134 @@ struct DevScene {
     const float *density;     // device copy of the grid (nx*ny*nz)
 };
 
-// host: derive per-quad constants exactly as oracle/ora_pbrt.h make_scene does; `d_density` is
-// the device copy of s->grid_density (grid media only)
+// host: derive the per-triangle constants and the light distribution exactly as
+// oracle/ora_pbrt.h make_scene does; `d_density` is the device copy of s->grid_density (grid media)
 void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density = nullptr);
 // host: GridDensityMedium ctor's maxDensity loop (grid.h:73-76), std::max order
 float grid_max_density(const bre_scene *s);
 
 struct Hit {
     f3 p, perr;
-    int quad;
+    int tri;
 };
 
-// one quad: plane solve, (u, v) in [0,1]^2, t in (0, tmax); hit point rebuilt on the quad with
-// the parallelogram form of the triangle error bound
-__device__ __forceinline__ bool intersect_quad(const PQuad &q, f3 o, f3 d, float tmax, float &t, Hit &h) {
-    const float denom = dot3(q.n, d);
-    if (denom == 0) return false;
-    t = dot3(q.n, sub3(q.p0, o)) / denom;
-    if (!(t > 0 && t < tmax)) return false;
-    const f3 rel = sub3(ray_at(o, d, t), q.p0);
-    const float u = dot3(rel, q.e1) * q.inv_e1sq;
-    const float v = dot3(rel, q.e2) * q.inv_e2sq;
-    if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) return false;
-    const f3 ue1 = scale3(q.e1, u), ve2 = scale3(q.e2, v);
-    h.p = add3(add3(q.p0, ue1), ve2);
-    h.perr = scale3(add3(add3(abs3(q.p0), abs3(ue1)), abs3(ve2)), gamma_n(6));
+BRE_TD int max_dim(f3 v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
+BRE_TD float comp(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+BRE_TD f3 permute3(f3 v, int x, int y, int z) { return mk(comp(v, x), comp(v, y), comp(v, z)); }
+BRE_TD float max_comp(f3 v) { return smax(v.x, smax(v.y, v.z)); }
+
+// Triangle::Intersect, triangle.cpp:177-300: the watertight test (translate to the ray origin,
+// permute so |d| is largest in z, shear, edge functions with a double-precision fallback on zero,
+// scaled t against tMax, conservative t > deltaT), then the barycentric hit point and its error bound
+__device__ __forceinline__ bool intersect_tri(const PTri &T, f3 o, f3 dir, float tmax, float &t, Hit &h) {
+    f3 p0t = sub3(T.p0, o), p1t = sub3(T.p1, o), p2t = sub3(T.p2, o);
+    const int kz = max_dim(abs3(dir));
+    int kx = kz + 1;
+    if (kx == 3) kx = 0;
+    int ky = kx + 1;
+    if (ky == 3) ky = 0;
+    const f3 d = permute3(dir, kx, ky, kz);
+    p0t = permute3(p0t, kx, ky, kz);
+    p1t = permute3(p1t, kx, ky, kz);
+    p2t = permute3(p2t, kx, ky, kz);
+    const float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1.f / d.z;
+    p0t.x += Sx * p0t.z;
+    p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z;
+    p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z;
+    p2t.y += Sy * p2t.z;
+    float e0 = p1t.x * p2t.y - p1t.y * p2t.x;
+    float e1 = p2t.x * p0t.y - p2t.y * p0t.x;
+    float e2 = p0t.x * p1t.y - p0t.y * p1t.x;
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        e0 = (float)((double)p2t.y * (double)p1t.x - (double)p2t.x * (double)p1t.y);
+        e1 = (float)((double)p0t.y * (double)p2t.x - (double)p0t.x * (double)p2t.y);
+        e2 = (float)((double)p1t.y * (double)p0t.x - (double)p1t.x * (double)p0t.y);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    const float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz;
+    p1t.z *= Sz;
+    p2t.z *= Sz;
+    const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tmax * det)) return false;
+    if (det > 0 && (tScaled <= 0 || tScaled > tmax * det)) return false;
+    const float invDet = 1 / det;
+    const float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    t = tScaled * invDet;
+    const float maxZt = max_comp(abs3(mk(p0t.z, p1t.z, p2t.z)));
+    const float deltaZ = gamma_n(3) * maxZt;
+    const float maxXt = max_comp(abs3(mk(p0t.x, p1t.x, p2t.x)));
+    const float maxYt = max_comp(abs3(mk(p0t.y, p1t.y, p2t.y)));
+    const float deltaX = gamma_n(5) * (maxXt + maxZt);
+    const float deltaY = gamma_n(5) * (maxYt + maxZt);
+    const float deltaE = 2 * (gamma_n(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    const float maxE = max_comp(abs3(mk(e0, e1, e2)));
+    const float deltaT = 3 * (gamma_n(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * fabsf(invDet);
+    if (t <= deltaT) return false;
+    const float xs = fabsf(b0 * T.p0.x) + fabsf(b1 * T.p1.x) + fabsf(b2 * T.p2.x);
+    const float ys = fabsf(b0 * T.p0.y) + fabsf(b1 * T.p1.y) + fabsf(b2 * T.p2.y);
+    const float zs = fabsf(b0 * T.p0.z) + fabsf(b1 * T.p1.z) + fabsf(b2 * T.p2.z);
+    h.perr = scale3(mk(xs, ys, zs), gamma_n(7));
+    h.p = add3(add3(scale3(T.p0, b0), scale3(T.p1, b1)), scale3(T.p2, b2));
     return true;
 }
 
-// closest hit over all quads; strict <, lowest index wins a tie; t in (0, tmax)
+// Scene::Intersect over the triangles in order: each hit shrinks tMax (primitive.cpp:97-101); the
+// reference's BVH order only decides exact ties (here the later triangle of equal t wins)
 __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, float &tmax, Hit &h) {
     bool hit = false;
-    for (int i = 0; i < S.n_quads; ++i) {
+    for (int i = 0; i < S.n_tris; ++i) {
         float t;
         Hit tmp;
-        if (!intersect_quad(S.q[i], o, d, tmax, t, tmp)) continue;
+        if (!intersect_tri(S.t[i], o, d, tmax, t, tmp)) continue;
         tmax = t;
         h.p = tmp.p;
         h.perr = tmp.perr;
-        h.quad = i;
+        h.tri = i;
         hit = true;
     }
     return hit;
+}
+
+// Triangle::Sample(u, pdf), triangle.cpp:543-568, with UniformSampleTriangle
+struct ShapeSample {
+    f3 p, perr, n;
+    float pdf;
+};
+BRE_TD ShapeSample sample_tri(const PTri &T, float u0, float u1) {
+    ShapeSample r;
+    const float su0 = sqrtf(u0);
+    const float b0 = 1 - su0, b1 = u1 * su0;
+    const float b2 = 1 - b0 - b1;
+    const f3 a = scale3(T.p0, b0), b = scale3(T.p1, b1), c = scale3(T.p2, b2);
+    r.p = add3(add3(a, b), c);
+    r.n = T.ns;
+    r.perr = scale3(add3(add3(abs3(a), abs3(b)), abs3(c)), gamma_n(6));
+    r.pdf = 1 / T.area;
+    return r;
+}
+
+// Distribution1D::SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389) over the
+// light powers; returns the light index (into light_tri)
+BRE_TD int sample_light(const DevScene &S, float u, float &pdf) {
+    const int size = S.n_lights + 1;
+    int first = 0, len = size;
+    while (len > 0) {
+        const int half = len >> 1, middle = first + half;
+        if (S.light_cdf[middle] <= u) {
+            first = middle + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    int off = first - 1;
+    off = off < 0 ? 0 : (off > size - 2 ? size - 2 : off);
+    pdf = (S.light_func_int > 0) ? S.light_func[off] / (S.light_func_int * (float)S.n_lights) : 0.f;
+    return off;
 }
 
 // Sampler draws: the photon pass draws from PCG32 (AwesomeHaltonSampler past its 1000 Halton

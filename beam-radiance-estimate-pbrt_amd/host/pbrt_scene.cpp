@@ -468,10 +468,8 @@ struct MediumDef {
 };
 
 struct ShapeRec {
-    bre_quad quad;
+    bre_triangle tri;
     std::string inside, outside;
-    bool emitter = false;
-    float L[3];
 };
 
 class Parser {
@@ -764,7 +762,7 @@ void Parser::MakeMedium(Lexer &lx, int line, const std::string &name, const Para
 
 void Parser::Shape(Lexer &lx, int line, const std::string &name, const ParamSet &ps) {
     if (name != "trianglemesh") {
-        Error(lx, line, "Shape \"%s\" is not supported (parallelogram \"trianglemesh\" only)", name.c_str());
+        Error(lx, line, "Shape \"%s\" is not supported (\"trianglemesh\" only)", name.c_str());
         return;
     }
     const std::vector<int> *idx = ps.FindInts("indices");
@@ -774,10 +772,11 @@ void Parser::Shape(Lexer &lx, int line, const std::string &name, const ParamSet 
         return;
     }
     for (const char *n : {"uv", "st", "N", "S", "alpha", "shadowalpha", "faceIndices"})
-        if (ps.Has(n)) Warning(lx, line, "trianglemesh \"%s\" is ignored by the quad scene model", n);
+        if (ps.Has(n)) Warning(lx, line, "trianglemesh \"%s\" is ignored by the GPU scene model", n);
     const size_t nv = P->size() / 3;
-    if (idx->size() % 6 != 0) {
-        Error(lx, line, "trianglemesh: %d indices do not pair into parallelograms (6 per quad)", (int)idx->size());
+    // CreateTriangleMeshShape (shapes/triangle.cpp): indices in triples
+    if (idx->size() % 3 != 0) {
+        Error(lx, line, "Number of vertex indices %d not a multiple of 3", (int)idx->size());
         return;
     }
     for (int i : *idx)
@@ -795,71 +794,34 @@ void Parser::Shape(Lexer &lx, int line, const std::string &name, const ParamSet 
         }
     }
     if (mat.none) {
-        Error(lx, line, "shapes without a material (medium boundaries) are not supported by the quad scene model");
+        Error(lx, line, "shapes without a material (medium boundaries) are not supported by the GPU scene model");
         return;
     }
-    // vertices to world space as Triangle does (ObjectToWorld(P[i]))
+    // vertices to world space as TriangleMesh does (mesh->p[i] = ObjectToWorld(P[i]))
     std::vector<float> W(P->size());
     for (size_t v = 0; v < nv; ++v) ctm_.ApplyPoint(&(*P)[3 * v], &W[3 * v]);
-    const size_t nquads = idx->size() / 6;
-    if (gs_.areaLight && nquads != 1) {
-        Error(lx, line, "an emitting trianglemesh must be exactly one parallelogram (2 triangles)");
-        return;
+    // Triangle::reverseOrientation ^ transformSwapsHandedness (Transform::SwapsHandedness: the
+    // determinant of the upper-left 3x3 is negative, transform.cpp)
+    float det = 0.f;
+    {
+        const float (*m)[4] = ctm_.m;
+        det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+              m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
     }
-    const bool flip = gs_.reverseOrientation;  // ^ transformSwapsHandedness: see below
-    for (size_t q = 0; q < nquads; ++q) {
-        const int *t1 = &(*idx)[6 * q], *t2 = &(*idx)[6 * q + 3];
-        int a = -1, b = -1, c = -1, d = -1;
-        for (int r = 0; r < 3 && a < 0; ++r) {
-            const int A = t1[r], B = t1[(r + 1) % 3], C = t1[(r + 2) % 3];
-            for (int s = 0; s < 3; ++s)
-                if (t2[s] == A && t2[(s + 1) % 3] == C) {  // second triangle (A C D) shares edge A-C
-                    a = A, b = B, c = C, d = t2[(s + 2) % 3];
-                    break;
-                }
-        }
-        if (a < 0) {
-            Error(lx, line, "trianglemesh triangles %d and %d do not share a diagonal with consistent winding",
-                  (int)(2 * q), (int)(2 * q + 1));
-            return;
-        }
-        const float *pa = &W[3 * a], *pb = &W[3 * b], *pc = &W[3 * c], *pd = &W[3 * d];
-        float mag = 0.f;
-        for (int k = 0; k < 3; ++k)
-            mag = std::max(mag, std::max(std::max(std::fabs(pa[k]), std::fabs(pb[k])), std::max(std::fabs(pc[k]), std::fabs(pd[k]))));
-        for (int k = 0; k < 3; ++k)
-            if (std::fabs((pb[k] + pd[k]) - (pa[k] + pc[k])) > 1e-5f * (mag + 1.f)) {
-                Error(lx, line, "trianglemesh quad %d is not a parallelogram", (int)q);
-                return;
-            }
+    const bool flip = gs_.reverseOrientation != (det < 0);
+    for (size_t t = 0; t < idx->size() / 3; ++t) {
         ShapeRec sr;
-        memset(&sr.quad, 0, sizeof(sr.quad));
-        for (int k = 0; k < 3; ++k) {
-            sr.quad.p0[k] = pa[k];
-            sr.quad.e1[k] = pb[k] - pa[k];  // dpdu of triangle (a b c) with pbrt's default uvs
-            sr.quad.e2[k] = pd[k] - pa[k];
-            sr.quad.kd[k] = mat.kd[k];
+        memset(&sr.tri, 0, sizeof(sr.tri));
+        for (int v = 0; v < 3; ++v) memcpy(sr.tri.p[v], &W[3 * (*idx)[3 * t + v]], 3 * sizeof(float));
+        memcpy(sr.tri.kd, mat.kd, sizeof(sr.tri.kd));
+        sr.tri.flip = flip ? 1 : 0;
+        if (gs_.areaLight) {
+            // pbrtShape: one DiffuseAreaLight per shape of the mesh (api.cpp), one-sided
+            sr.tri.emit = 1;
+            memcpy(sr.tri.Le, gs_.areaL, sizeof(sr.tri.Le));
         }
         sr.inside = gs_.inside;
         sr.outside = gs_.outside;
-        if (gs_.areaLight) {
-            // DiffuseAreaLight is one-sided: its side is the shape normal, which pbrt flips under
-            // ReverseOrientation ^ TransformSwapsHandedness; the quad normal is e1 x e2
-            float det = 0.f;
-            {
-                const float (*m)[4] = ctm_.m;
-                det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
-                      m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
-                      m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
-            }
-            if (flip != (det < 0)) {
-                // flip the facing by swapping the edges (normal e2 x e1 = -(e1 x e2))
-                for (int k = 0; k < 3; ++k) std::swap(sr.quad.e1[k], sr.quad.e2[k]);
-                Warning(lx, line, "emitter orientation flipped: its shading tangent becomes the other edge");
-            }
-            sr.emitter = true;
-            memcpy(sr.L, gs_.areaL, sizeof(sr.L));
-        }
         shapes_.push_back(sr);
     }
     ReportUnused(lx, line, ps);
@@ -1030,7 +992,7 @@ bool Parser::Run(Lexer &lx, int depth) {
         } else if (w == "ObjectBegin" || w == "ObjectInstance") {
             std::string n;
             if (!str(&n)) break;
-            Error(lx, line, "%s is not supported by the quad scene model", w.c_str());
+            Error(lx, line, "%s is not supported by the GPU scene model", w.c_str());
         } else if (w == "ObjectEnd") {
         } else if (w == "Camera" || w == "Film" || w == "Sampler" || w == "PixelFilter" || w == "Accelerator" ||
                    w == "Integrator" || w == "Shape" || w == "Material" || w == "LightSource" ||
@@ -1079,7 +1041,7 @@ bool Parser::Run(Lexer &lx, int depth) {
                     namedMaterials_[n] = m;
                 }
             } else if (w == "LightSource") {
-                Error(lx, line, "LightSource \"%s\" is not supported (one diffuse area light only)", n.c_str());
+                Error(lx, line, "LightSource \"%s\" is not supported (diffuse area lights only)", n.c_str());
             } else if (w == "AreaLightSource") {
                 if (n != "diffuse" && n != "area") {
                     Error(lx, line, "AreaLightSource \"%s\" unknown", n.c_str());
@@ -1098,7 +1060,7 @@ bool Parser::Run(Lexer &lx, int depth) {
             } else if (w == "MakeNamedMedium") {
                 MakeMedium(lx, line, n, ps);
             } else if (w == "Texture") {
-                Error(lx, line, "textures are not supported by the quad scene model");
+                Error(lx, line, "textures are not supported by the GPU scene model");
             }
         } else {
             err = "unknown directive \"" + w + "\"";
@@ -1119,14 +1081,11 @@ bool Parser::Finish() {
     };
     if (!o.haveCamera) return fatal("no usable perspective Camera");
     if (shapes_.empty()) return fatal("the scene has no shapes");
-    if ((int)shapes_.size() > BRE_MAX_QUADS) return fatal("more than BRE_MAX_QUADS parallelograms");
-    int nemit = 0, light = -1;
-    for (size_t i = 0; i < shapes_.size(); ++i)
-        if (shapes_[i].emitter) {
-            ++nemit;
-            light = (int)i;
-        }
-    if (nemit != 1) return fatal("the scene model needs exactly one diffuse area light (found " + std::to_string(nemit) + ")");
+    if ((int)shapes_.size() > BRE_MAX_TRIANGLES)
+        return fatal("more than BRE_MAX_TRIANGLES (" + std::to_string(BRE_MAX_TRIANGLES) + ") triangles");
+    int nemit = 0;
+    for (size_t i = 0; i < shapes_.size(); ++i) nemit += shapes_[i].tri.emit != 0;
+    if (nemit == 0) return fatal("the scene has no diffuse area light");
     // The camera medium is the outside medium of the graphics state at WorldEnd (api.cpp:651-655).
     const std::string M = gs_.outside;
     const MediumDef *med = nullptr;
@@ -1142,16 +1101,14 @@ bool Parser::Finish() {
         const ShapeRec &s = shapes_[i];
         const bool inherit = s.inside.empty() && s.outside.empty();
         const bool same = s.inside == M && s.outside == M;
-        if (s.emitter ? !same : !(inherit || same))
+        if (s.tri.emit ? !same : !(inherit || same))
             return fatal("shape " + std::to_string(i) + " has MediumInterface \"" + s.inside + "\" \"" + s.outside +
                          "\"; the GPU scene model has one medium (\"" + M + "\") filling all space");
     }
     bre_scene &sc = o.scene;
     memset(&sc, 0, sizeof(sc));
-    sc.n_quads = (int32_t)shapes_.size();
-    for (size_t i = 0; i < shapes_.size(); ++i) sc.quads[i] = shapes_[i].quad;
-    sc.light_quad = light;
-    memcpy(sc.light_L, shapes_[light].L, sizeof(sc.light_L));
+    sc.n_triangles = (int32_t)shapes_.size();
+    for (size_t i = 0; i < shapes_.size(); ++i) sc.triangles[i] = shapes_[i].tri;
     if (med) {
         sc.has_medium = med->kind;
         memcpy(sc.sigma_a, med->sigma_a, sizeof(sc.sigma_a));

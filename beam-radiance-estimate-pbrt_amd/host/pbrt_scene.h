@@ -14,11 +14,12 @@
 //
 // What the subset accepts is what the GPU scene model (include/bre_scene.h) can render; anything
 // else is reported with pbrt-style Error()/Warning() text and the offending statement skipped:
-//   * Shape "trianglemesh" whose triangles pair into parallelograms -> bre_quad (p0 = v0,
-//     e1 = v1 - v0, e2 = v3 - v0 for triangles (v0 v1 v2)(v0 v2 v3)); vertices go through the
-//     CTM exactly as Triangle does (ObjectToWorld(P[i]), shapes/triangle.cpp).
+//   * Shape "trianglemesh" -> one bre_triangle per index triple (vertices through the CTM exactly
+//     as TriangleMesh does, mesh->p[i] = ObjectToWorld(P[i]), shapes/triangle.cpp; flip =
+//     ReverseOrientation ^ TransformSwapsHandedness); up to BRE_MAX_TRIANGLES.
 //   * Material "matte" with "Kd" (rgb, default 0.5) and sigma 0; MakeNamedMaterial/NamedMaterial.
-//   * one AreaLightSource "diffuse" ("L" x "scale", one-sided) on one parallelogram.
+//   * AreaLightSource "diffuse" ("L" x "scale", one-sided): every triangle of an emitting mesh is
+//     its own light, as pbrtShape makes one DiffuseAreaLight per shape (api.cpp).
 //   * media: "homogeneous" or "heterogeneous" (GridDensityMedium); the scene model has ONE medium
 //     filling all space, so every shape's inside/outside medium and the camera medium must be
 //     that medium (or all empty = vacuum).
@@ -29,7 +30,7 @@
 //     film image directly (Film::SetImage), so neither the scene's sampler nor filter is used.
 //   * Include "file" (relative to the including file), comments, AttributeBegin/End,
 //     TransformBegin/End, Translate, Scale, Rotate, LookAt, Transform, ConcatTransform,
-//     CoordinateSystem, CoordSysTransform, ReverseOrientation (rejected on emitters: one-sided).
+//     CoordinateSystem, CoordSysTransform, ReverseOrientation.
 #pragma once
 
 #include <map>

@@ -8,22 +8,23 @@ from __future__ import annotations
 
 import ctypes
 
-MAX_QUADS = 64
+MAX_TRIANGLES = 128
 MAX_DEPTH = 16
 MEDIUM_NONE, MEDIUM_HOMOGENEOUS, MEDIUM_GRID = 0, 1, 2
 
 F3 = ctypes.c_float * 3
 
 
-class Quad(ctypes.Structure):
-    _fields_ = [("p0", F3), ("e1", F3), ("e2", F3), ("kd", F3)]
+class Triangle(ctypes.Structure):
+    """bre_triangle: one pbrt Triangle (world-space vertices in mesh index order)."""
+    _fields_ = [("p", F3 * 3), ("kd", F3), ("Le", F3), ("emit", ctypes.c_int32), ("flip", ctypes.c_int32)]
 
 
 class Scene(ctypes.Structure):
-    _fields_ = [("n_quads", ctypes.c_int32), ("light_quad", ctypes.c_int32), ("light_L", F3),
+    _fields_ = [("n_triangles", ctypes.c_int32),
                 ("has_medium", ctypes.c_int32), ("sigma_a", F3), ("sigma_s", F3), ("g", ctypes.c_float),
                 ("cam_pos", F3), ("cam_look", F3), ("cam_up", F3), ("cam_fov_deg", ctypes.c_float),
-                ("quads", Quad * MAX_QUADS),
+                ("triangles", Triangle * MAX_TRIANGLES),
                 ("grid_n", ctypes.c_int32 * 3), ("world_to_medium", ctypes.c_float * 16),
                 ("grid_density", ctypes.c_void_p)]
 
@@ -52,17 +53,27 @@ def _f3(v):
     return F3(*[float(x) for x in v])
 
 
-def make_scene(quads, light_quad, light_L, sigma_a=None, sigma_s=None, g=0.0,
+def make_scene(meshes, sigma_a=None, sigma_s=None, g=0.0,
                cam_pos=(0.5, 0.5, 0.02), cam_look=(0.5, 0.5, 1.0), cam_up=(0.0, 1.0, 0.0), fov=60.0) -> Scene:
-    """quads: list of (p0, e1, e2, kd); medium present iff sigma_a is given (RGB or scalar)."""
+    """meshes: list of (P, indices, kd, Le) -- a pbrt "trianglemesh" with world-space points P
+    (list of xyz), index triples, Lambertian kd, and Le (None = not emitting); medium present iff
+    sigma_a is given (RGB or scalar)."""
     s = Scene()
     ctypes.memset(ctypes.addressof(s), 0, ctypes.sizeof(s))
-    assert 1 <= len(quads) <= MAX_QUADS
-    s.n_quads = len(quads)
-    for i, (p0, e1, e2, kd) in enumerate(quads):
-        s.quads[i].p0, s.quads[i].e1, s.quads[i].e2, s.quads[i].kd = _f3(p0), _f3(e1), _f3(e2), _f3(kd)
-    s.light_quad = light_quad
-    s.light_L = _f3(light_L)
+    n = 0
+    for P, idx, kd, Le in meshes:
+        assert len(idx) % 3 == 0
+        for t in range(len(idx) // 3):
+            assert n < MAX_TRIANGLES
+            T = s.triangles[n]
+            for v in range(3):
+                T.p[v] = _f3(P[idx[3 * t + v]])
+            T.kd = _f3(kd)
+            if Le is not None:
+                T.emit = 1
+                T.Le = _f3(Le)
+            n += 1
+    s.n_triangles = n
     if sigma_a is not None:
         rgb = (lambda v: (v, v, v) if isinstance(v, (int, float)) else tuple(v))
         s.has_medium = 1
@@ -77,24 +88,27 @@ def make_scene(quads, light_quad, light_L, sigma_a=None, sigma_s=None, g=0.0,
 WHITE = (0.73, 0.73, 0.73)
 RED = (0.63, 0.065, 0.05)
 GREEN = (0.14, 0.45, 0.091)
+QUAD = (0, 1, 2, 0, 2, 3)  # scenes/cornell_world.pbrt: "integer indices" [0 1 2 0 2 3]
 
 
-def cornell_quads():
-    """Unit-cube Cornell box, normals inward (normal = normalize(e1 x e2)); light last."""
+def cornell_meshes(light_L=(17.0, 12.0, 4.0)):
+    """scenes/cornell_world.pbrt: unit-cube Cornell box, one two-triangle mesh per wall (normals
+    inward), the area light last (facing down)."""
     return [
-        ((0, 0, 0), (0, 0, 1), (1, 0, 0), WHITE),     # floor
-        ((0, 1, 0), (1, 0, 0), (0, 0, 1), WHITE),     # ceiling
-        ((0, 0, 1), (0, 1, 0), (1, 0, 0), WHITE),     # back wall
-        ((0, 0, 0), (1, 0, 0), (0, 1, 0), WHITE),     # front wall (behind the camera)
-        ((0, 0, 0), (0, 1, 0), (0, 0, 1), RED),       # left wall
-        ((1, 0, 0), (0, 0, 1), (0, 1, 0), GREEN),     # right wall
-        ((0.35, 0.999, 0.35), (0.3, 0, 0), (0, 0, 0.3), (0, 0, 0)),  # area light, facing down
+        ([(0, 0, 0), (0, 0, 1), (1, 0, 1), (1, 0, 0)], QUAD, WHITE, None),     # floor
+        ([(0, 1, 0), (1, 1, 0), (1, 1, 1), (0, 1, 1)], QUAD, WHITE, None),     # ceiling
+        ([(0, 0, 1), (0, 1, 1), (1, 1, 1), (1, 0, 1)], QUAD, WHITE, None),     # back wall
+        ([(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0)], QUAD, WHITE, None),     # front wall (behind the camera)
+        ([(0, 0, 0), (0, 1, 0), (0, 1, 1), (0, 0, 1)], QUAD, RED, None),       # left wall
+        ([(1, 0, 0), (1, 0, 1), (1, 1, 1), (1, 1, 0)], QUAD, GREEN, None),     # right wall
+        ([(0.35, 0.999, 0.35), (0.65, 0.999, 0.35), (0.65, 0.999, 0.65), (0.35, 0.999, 0.65)], QUAD, (0, 0, 0),
+         light_L),                                                            # area light
     ]
 
 
 def cornell_scene(sigma_a: float = 0.05, sigma_s: float = 0.5, g: float = 0.0) -> Scene:
     """Cornell box in homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)."""
-    return make_scene(cornell_quads(), 6, (17.0, 12.0, 4.0), sigma_a, sigma_s, g)
+    return make_scene(cornell_meshes(), sigma_a, sigma_s, g)
 
 
 def smoke_density(n: int = 64, seed: int = 7):

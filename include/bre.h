@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define BRE_ABI_VERSION 1
+#define BRE_ABI_VERSION 2 /* 2: triangle scene model (bre_scene.h) */
 
 typedef struct bre_ctx bre_ctx;
 

@@ -6,16 +6,22 @@
  * src/integrators/photonbeam.cpp:258-325, 383-421) and the camera pass
  * (photonbeam.cpp:456-555) can run on the GPU next to the gather.
  *
- * The scene model is deliberately the subset the benchmark scene of SURVEY.md §8d (C1/C2: a
- * Cornell box of matte quads, one diffuse area light, a homogeneous fog filling the box, a
- * pinhole camera inside the fog) needs:
- *   - bre_quad          parallelograms p0 + u*e1 + v*e2, u,v in [0,1], with a Lambertian
- *                       reflectance (MatteMaterial with sigma 0, src/materials/matte.cpp;
+ * The scene model is the subset of pbrt-v3 the benchmark scenes of SURVEY.md §8d need, kept at
+ * pbrt's own granularity so every random decision and every float matches the reference:
+ *   - bre_triangle      one pbrt Triangle of a "trianglemesh" (src/shapes/triangle.cpp): its three
+ *                       world-space vertices in the mesh's index order, hit by the watertight
+ *                       Triangle::Intersect (:177-300), with the triangle's own geometric normal
+ *                       normalize(cross(p0 - p2, p1 - p2)) and shading frame ss = normalize(p1 - p0)
+ *                       (dpdu for pbrt's default (0,0), (1,0), (1,1) uvs, :276-294), and a
+ *                       Lambertian reflectance (MatteMaterial with sigma 0, src/materials/matte.cpp;
  *                       black kd = no BxDF, so a photon hitting it is absorbed,
- *                       reflection.cpp:708-713).  Geometric = shading normal =
- *                       normalize(e1 x e2); the shading tangent ss = normalize(e1).
- *   - one diffuse area light (DiffuseAreaLight, one-sided, src/lights/diffuse.cpp:89-123) on
- *                       quad `light_quad`, emitting light_L towards +normal.
+ *                       reflection.cpp:708-713).  `flip` = ReverseOrientation ^
+ *                       TransformSwapsHandedness (the normal is negated, :296-297).
+ *   - diffuse area lights: every triangle with `emit` set is its own one-sided DiffuseAreaLight
+ *                       (src/lights/diffuse.cpp:89-123; pbrtShape makes one light per shape of an
+ *                       emitting mesh, api.cpp), in triangle order = scene.lights order.  The photon
+ *                       pass picks one by power (ComputeLightPowerDistribution,
+ *                       integrator.cpp:217-225); the camera pass uniformly (UniformSampleOneLight).
  *   - an optional medium filling all of space (every ray -- camera, photon, spawned -- travels
  *                       in it) with a Henyey-Greenstein phase function (src/core/medium.cpp:194-213):
  *                       BRE_MEDIUM_HOMOGENEOUS = HomogeneousMedium (src/media/homogeneous.cpp:44-77),
@@ -24,8 +30,8 @@
  *                       tracking (Sample) and ratio tracking with Russian roulette (Tr); both draw
  *                       from the path's sampler.  sigma_a + sigma_s must be spectrally uniform.
  *   - a perspective pinhole camera (src/cameras/perspective.cpp, lensradius 0).
- * Geometry contract shared by the GPU pass and the oracle (both evaluate it with IEEE float,
- * no FMA contraction): see DESIGN.md "Photon pass".
+ * The GPU passes and the oracle evaluate it with IEEE float, no FMA contraction (DESIGN.md
+ * "Photon pass").
  */
 #ifndef BRE_SCENE_H
 #define BRE_SCENE_H
@@ -36,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BRE_MAX_QUADS 64
+#define BRE_MAX_TRIANGLES 128
 #define BRE_MAX_DEPTH 16 /* maxdepth accepted by the photon / camera passes */
 
 #define BRE_MEDIUM_NONE 0
@@ -44,17 +50,16 @@ extern "C" {
 #define BRE_MEDIUM_GRID 2
 #define BRE_MAX_GRID_CELLS (1 << 26) /* nx*ny*nz accepted for a GridDensityMedium */
 
-typedef struct bre_quad {
-    float p0[3]; /* corner */
-    float e1[3]; /* edge u (shading tangent direction) */
-    float e2[3]; /* edge v; normal = normalize(e1 x e2) */
-    float kd[3]; /* Lambertian reflectance; all-zero = absorbing (no BxDF) */
-} bre_quad;
+typedef struct bre_triangle {
+    float p[3][3]; /* world-space vertices mesh->p[v[0..2]] (ObjectToWorld applied) */
+    float kd[3];   /* Lambertian reflectance; all-zero = absorbing (no BxDF) */
+    float Le[3];   /* DiffuseAreaLight "L" (Lemit) when emit != 0 */
+    int32_t emit;  /* 1: a one-sided diffuse area light */
+    int32_t flip;  /* 1: ReverseOrientation ^ TransformSwapsHandedness (normal negated) */
+} bre_triangle;
 
 typedef struct bre_scene {
-    int32_t n_quads;       /* 1 .. BRE_MAX_QUADS */
-    int32_t light_quad;    /* index of the emitting quad */
-    float light_L[3];      /* DiffuseAreaLight "L" (Lemit) */
+    int32_t n_triangles;   /* 1 .. BRE_MAX_TRIANGLES; at least one with emit != 0 */
     int32_t has_medium;    /* BRE_MEDIUM_NONE (vacuum) / _HOMOGENEOUS / _GRID, filling all space */
     float sigma_a[3];      /* medium sigma_a (already multiplied by "scale") */
     float sigma_s[3];      /* medium sigma_s */
@@ -63,7 +68,7 @@ typedef struct bre_scene {
     float cam_look[3];     /* LookAt target */
     float cam_up[3];       /* LookAt up */
     float cam_fov_deg;     /* perspective "fov" (degrees, spans the shorter image axis) */
-    bre_quad quads[BRE_MAX_QUADS];
+    bre_triangle triangles[BRE_MAX_TRIANGLES];
     /* GridDensityMedium only (has_medium == BRE_MEDIUM_GRID; MakeMedium "heterogeneous",
        api.cpp:547-593): */
     int32_t grid_n[3];          /* nx, ny, nz (each >= 1, product <= BRE_MAX_GRID_CELLS) */
@@ -87,10 +92,11 @@ typedef struct bre_render_params {
     float alpha;                    /* "alpha" (default 0.5) */
 } bre_render_params;
 
-/* The benchmark scene of SURVEY.md §8d (C1/C2): unit-cube Cornell box (white floor, ceiling and
-   back wall, red left wall, green right wall, white front wall behind the camera), a 0.3 x 0.3
-   area light just below the ceiling facing down, homogeneous fog sigma_a, sigma_s (grey), HG g,
-   camera at (0.5, 0.5, 0.02) looking at (0.5, 0.5, 1) with a 60 degree field of view. */
+/* The benchmark scene of SURVEY.md §8d (C1/C2), scenes/cornell_world.pbrt: unit-cube Cornell box
+   (white floor, ceiling and back wall, red left wall, green right wall, white front wall behind
+   the camera), a 0.3 x 0.3 area light just below the ceiling facing down, each wall one
+   "trianglemesh" of two triangles (v0 v1 v2)(v0 v2 v3), homogeneous fog sigma_a, sigma_s (grey),
+   HG g, camera at (0.5, 0.5, 0.02) looking at (0.5, 0.5, 1) with a 60 degree field of view. */
 void bre_scene_cornell(bre_scene *scene, float sigma_a, float sigma_s, float g);
 
 /* SURVEY.md §8d C3/C5 smoke: the same Cornell box with a GridDensityMedium of sigma_a, sigma_s

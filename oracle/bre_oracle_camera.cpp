@@ -272,13 +272,13 @@ static Ray GenerateRay(const Camera &c, Float fx, Float fy) {
     return r;
 }
 
-// ---- BSDF of a matte quad (reflection.cpp:650-768) ----
-static inline V3 WorldToLocal(const Quad &q, const V3 &v) { return V3(Dot(v, q.ss), Dot(v, q.ts), Dot(v, q.n)); }
-static inline V3 LocalToWorld(const Quad &q, const V3 &v) {
+// ---- BSDF of a matte triangle (reflection.cpp:650-768) ----
+static inline V3 WorldToLocal(const Tri &q, const V3 &v) { return V3(Dot(v, q.ss), Dot(v, q.ts), Dot(v, q.n)); }
+static inline V3 LocalToWorld(const Tri &q, const V3 &v) {
     return V3(q.ss.x * v.x + q.ts.x * v.y + q.n.x * v.z, q.ss.y * v.x + q.ts.y * v.y + q.n.y * v.z,
               q.ss.z * v.x + q.ts.z * v.y + q.n.z * v.z);
 }
-static Spectrum BSDF_f(const Quad &q, const V3 &woW, const V3 &wiW) {
+static Spectrum BSDF_f(const Tri &q, const V3 &woW, const V3 &wiW) {
     if (q.kd.IsBlack()) return Spectrum(0.f);  // no BxDF
     V3 wo = WorldToLocal(q, woW);
     if (wo.z == 0) return Spectrum(0.f);
@@ -287,7 +287,7 @@ static Spectrum BSDF_f(const Quad &q, const V3 &woW, const V3 &wiW) {
     if (reflect) f = f + q.kd * InvPi;
     return f;
 }
-static Float BSDF_Pdf(const Quad &q, const V3 &woW, const V3 &wiW) {
+static Float BSDF_Pdf(const Tri &q, const V3 &woW, const V3 &wiW) {
     if (q.kd.IsBlack()) return 0.f;
     V3 wo = WorldToLocal(q, woW), wi = WorldToLocal(q, wiW);
     if (wo.z == 0) return 0.;
@@ -296,7 +296,7 @@ static Float BSDF_Pdf(const Quad &q, const V3 &woW, const V3 &wiW) {
     return pdf / 1;
 }
 // returns f; *pdf untouched when wo.z == 0 (as the reference)
-static Spectrum BSDF_Sample_f(const Quad &q, const V3 &woW, V3 *wiW, Float ux, Float uy, Float *pdf) {
+static Spectrum BSDF_Sample_f(const Tri &q, const V3 &woW, V3 *wiW, Float ux, Float uy, Float *pdf) {
     if (q.kd.IsBlack()) {
         *pdf = 0;
         return Spectrum(0.f);
@@ -320,7 +320,7 @@ static inline Float PowerHeuristic(int nf, Float fPdf, int ng, Float gPdf) {
 
 struct Interaction {
     V3 p, pError, n, wo;
-    int quad;
+    int tri;
 };
 
 static Spectrum VisibilityTr(const Scene &sc, const Interaction &p0, const Interaction &p1, CameraSampler &cs) {
@@ -332,25 +332,26 @@ static Spectrum VisibilityTr(const Scene &sc, const Interaction &p0, const Inter
     Spectrum Tr(1.f);
     Isect isect;
     bool hit = Intersect(sc, ray, &isect);
-    if (hit) return Spectrum(0.0f);  // every quad has a material
+    if (hit) return Spectrum(0.0f);  // every triangle has a material
     if (sc.medium) Tr = Tr * MediumTr(sc, ray, cs);
     return Tr;
 }
 
-static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx, Float usy, Float ulx, Float uly,
-                               CameraSampler &cs) {
-    const Quad &L = sc.quads[sc.light];
-    const Quad &q = sc.quads[it.quad];
+// EstimateDirect (integrator.cpp:99-199) for the area light on triangle `li` (handleMedia = true)
+static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, int li, Float usx, Float usy, Float ulx,
+                               Float uly, CameraSampler &cs) {
+    const Tri &L = sc.tris[li];
+    const Tri &q = sc.tris[it.tri];
     Spectrum Ld(0.f);
     V3 wi;
     Float lightPdf = 0, scatteringPdf = 0;
-    // DiffuseAreaLight::Sample_Li -> Shape::Sample(ref, u)
+    // DiffuseAreaLight::Sample_Li (diffuse.cpp:68-81) -> Shape::Sample(ref, u) (shape.cpp:56-70)
+    const ShapeSample ss = SampleTri(L, ulx, uly);
     Interaction pS;
-    V3 ue1 = L.e1 * ulx, ve2 = L.e2 * uly;
-    pS.p = L.p0 + ue1 + ve2;
-    pS.pError = (Abs(L.p0) + Abs(ue1) + Abs(ve2)) * gamma(6);
-    pS.n = L.n;
-    lightPdf = 1 / L.area;
+    pS.p = ss.p;
+    pS.pError = ss.pError;
+    pS.n = ss.n;
+    lightPdf = ss.pdf;
     V3 w = pS.p - it.p;
     if (w.LengthSquared() == 0) {
         lightPdf = 0;
@@ -364,7 +365,7 @@ static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx
         lightPdf = 0;
     } else {
         wi = Normalize(pS.p - it.p);
-        Li = Dot(pS.n, -wi) > 0 ? sc.Lemit : Spectrum(0.f);
+        Li = Dot(pS.n, -wi) > 0 ? L.Le : Spectrum(0.f);
     }
     if (lightPdf > 0 && !Li.IsBlack()) {
         Spectrum f = BSDF_f(q, it.wo, wi) * AbsDot(wi, q.n);
@@ -382,14 +383,14 @@ static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx
         Spectrum f = BSDF_Sample_f(q, it.wo, &wi, usx, usy, &scatteringPdf);
         f = f * AbsDot(wi, q.n);
         if (!f.IsBlack() && scatteringPdf > 0) {
-            // DiffuseAreaLight::Pdf_Li -> Shape::Pdf(ref, wi): intersect the light's shape alone
+            // DiffuseAreaLight::Pdf_Li -> Shape::Pdf(ref, wi) (shape.cpp:72-87): this triangle alone
             Ray ray;
             ray.o = OffsetRayOrigin(it.p, it.pError, it.n, wi);
             ray.d = wi;
             ray.tMax = Infinity;
             Float tHit;
             Isect isL;
-            if (!IntersectQuad(L, ray, &tHit, &isL)) return Ld;
+            if (!IntersectTri(L, ray, &tHit, &isL)) return Ld;
             lightPdf = (it.p - isL.p).LengthSquared() / (AbsDot(isL.n, -wi) * L.area);
             if (std::isinf(lightPdf)) lightPdf = 0.f;
             if (lightPdf == 0) return Ld;
@@ -400,11 +401,12 @@ static Spectrum EstimateDirect(const Scene &sc, const Interaction &it, Float usx
             r2.d = wi;
             r2.tMax = Infinity;
             Spectrum Tr(1.f);
-            Isect li;
-            bool found = Intersect(sc, r2, &li);
+            Isect lh;
+            bool found = Intersect(sc, r2, &lh);
             if (sc.medium) Tr = Tr * MediumTr(sc, r2, cs);
             Spectrum Lr(0.f);
-            if (found && li.quad == sc.light) Lr = Dot(li.n, -wi) > 0 ? sc.Lemit : Spectrum(0.f);
+            // lightIsect.primitive->GetAreaLight() == &light: the same triangle
+            if (found && lh.tri == li) Lr = Dot(lh.n, -wi) > 0 ? L.Le : Spectrum(0.f);
             if (!Lr.IsBlack()) Ld = Ld + f * Lr * Tr * weight / scatteringPdf;
         }
     }
@@ -436,6 +438,7 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
     Spectrum beta(1.f);
     bool specularBounce = false;
     const int pixel = py * width + px;
+    const int nLights = (int)sc.lights.size();
     for (int depth = 0; depth < maxDepth; ++depth) {
         Isect isect;
         ray.tMax = Infinity;
@@ -444,13 +447,16 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
         if (sc.medium) mediumBeta = MediumTr(sc, ray, cs);
         if (renderMedia) segs.push_back(Segment{ray.o, isect.p, ray.d, ray.tMax, pixel, depth});
         beta = beta * mediumBeta;
-        if (!renderSurfaces) break;  // every quad has a BSDF
-        const Quad &q = sc.quads[isect.quad];
+        if (!renderSurfaces) break;  // every triangle has a BSDF
+        const Tri &q = sc.tris[isect.tri];
         V3 wo = -ray.d;
+        // isect.Le(wo): the triangle's own area light, one-sided (diffuse.h:56-58)
         if (depth == 0 || specularBounce)
-            if (isect.quad == sc.light) *Ld = *Ld + beta * (Dot(isect.n, wo) > 0 ? sc.Lemit : Spectrum(0.f));
-        // UniformSampleOneLight (one light: lightPdf = 1)
-        cs.Get1D();
+            if (q.emit) *Ld = *Ld + beta * (Dot(isect.n, wo) > 0 ? q.Le : Spectrum(0.f));
+        // UniformSampleOneLight (integrator.cpp:54-82), no light distribution: uniform choice
+        const Float ul = cs.Get1D();
+        const int lightNum = std::min((int)(ul * nLights), nLights - 1);
+        const Float lightPdf = Float(1) / nLights;
         Float ulx, uly, usx, usy;
         cs.Get2D(&ulx, &uly);
         cs.Get2D(&usx, &usy);
@@ -459,8 +465,8 @@ static bool CameraPath(const Scene &sc, const Camera &cam, const Halton &h, int 
         it.pError = isect.pError;
         it.n = isect.n;
         it.wo = Normalize(wo);
-        it.quad = isect.quad;
-        *Ld = *Ld + beta * (EstimateDirect(sc, it, usx, usy, ulx, uly, cs) / Float(1));
+        it.tri = isect.tri;
+        *Ld = *Ld + beta * (EstimateDirect(sc, it, sc.lights[lightNum], usx, usy, ulx, uly, cs) / lightPdf);
         if (depth < maxDepth - 1) {
             Float ux, uy, pdf = 0;
             cs.Get2D(&ux, &uy);

@@ -32,11 +32,14 @@
 //     constructor arguments right to left on x86-64 (checked with this image's g++ on a
 //     stand-alone snippet), so x = second draw, y = first draw.
 //   * Transcendentals (log, exp, sin, cos) come from include/bre_fmath.h on both sides, so the
-//     GPU pass and this restatement agree bit for bit; they are within 2 ulp of libm.
-//   * Scene geometry (quads instead of pbrt triangle meshes): see include/bre_scene.h and
-//     DESIGN.md "Photon pass".  Ray-quad hit: plane solve, (u, v) test, point rebuilt on the quad
-//     as p0 + u*e1 + v*e2 with pError = gamma(6)*(|p0| + |u*e1| + |v*e2|) (the triangle form of
-//     src/shapes/triangle.cpp's error bound, two edges instead of three vertices).
+//     GPU pass and this restatement agree bit for bit; they are within 2 ulp of libm.  With
+//     ora_set_libm(1) the oracle uses the host libm instead, as the reference does
+//     (tests/test_faithful.py measures what that changes).
+//   * Scene geometry: pbrt Triangles (include/bre_scene.h) -- Triangle::Intersect (watertight,
+//     src/shapes/triangle.cpp:177-300), Triangle::Sample / Area (:535-568), one DiffuseAreaLight per
+//     emitting triangle chosen by power (ComputeLightPowerDistribution, integrator.cpp:217-225;
+//     Distribution1D::SampleDiscrete, sampling.h:55-100).  Scene::Intersect visits the triangles
+//     in order (the reference's BVH order only matters for exact ties).
 //
 // Parity status: the photon pass has no reference test, golden vector or fixture
 // and the reference cannot be built here: UNPINNED except for the primitives
@@ -86,7 +89,7 @@ static void TraceRecursive(Ray photonRay, int depth, Spectrum beta, Sampler &sam
         out.push_back(b);
 
         // BSDF (MatteMaterial -> one LambertianReflection, or none when kd is black)
-        const Quad &q = sc.quads[isect.quad];
+        const Tri &q = sc.tris[isect.tri];
         Float u0, u1;
         sampler.Get2D(&u0, &u1);  // evaluated before Sample_f runs
         if (q.kd.IsBlack()) break;  // matchingComps == 0: f = 0, pdf = 0
@@ -110,39 +113,46 @@ static void TraceRecursive(Ray photonRay, int depth, Spectrum beta, Sampler &sam
     }
 }
 
-// Emission (photonbeam.cpp:383-421) with a single light (lightPdf = 1)
+// Emission (photonbeam.cpp:383-421): the light by power (lightDistr->SampleDiscrete), then
+// DiffuseAreaLight::Sample_Le (diffuse.cpp:89-123) on its triangle (Triangle::Sample)
 static void TracePhoton(const Scene &sc, uint64_t seq, int MaxDepth, Float BeamRadius, std::vector<Beam> &out) {
     Sampler sampler(seq);
-    sampler.Get1D();  // lightSample: one light, SampleDiscrete returns 0 with pdf 1
-    const Float lightPdf = 1;
+    Float lightPdf;
+    const int lightNum = SampleDiscrete(sc, sampler.Get1D(), &lightPdf);
+    const Tri &L = sc.tris[sc.lights[lightNum]];
     Float u0x, u0y, u1x, u1y;
     sampler.Get2D(&u0x, &u0y);
     sampler.Get2D(&u1x, &u1y);
     sampler.Get1D();  // uLightTime (shutter is [0,0])
-    const Quad &L = sc.quads[sc.light];
-    // Shape::Sample: uniform point on the parallelogram
-    V3 ue1 = L.e1 * u0x, ve2 = L.e2 * u0y;
-    V3 p = L.p0 + ue1 + ve2;
-    V3 pError = (Abs(L.p0) + Abs(ue1) + Abs(ve2)) * gamma(6);
-    Float pdfPos = 1 / L.area;
-    V3 nLight = L.n;
+    const ShapeSample ps = SampleTri(L, u0x, u0y);
+    const Float pdfPos = ps.pdf;
+    const V3 nLight = ps.n;
     V3 w = CosineSampleHemisphere(u1x, u1y);
     Float pdfDir = w.z * InvPi;
     V3 v1, v2;
     CoordinateSystem(nLight, &v1, &v2);
     w = w.x * v1 + w.y * v2 + w.z * nLight;
     Ray ray;
-    ray.o = OffsetRayOrigin(p, pError, nLight, w);
+    ray.o = OffsetRayOrigin(ps.p, ps.pError, nLight, w);
     ray.d = w;
     ray.tMax = Infinity;
-    Spectrum Le = Dot(nLight, w) > 0 ? sc.Lemit : Spectrum(0.f);
+    Spectrum Le = Dot(nLight, w) > 0 ? L.Le : Spectrum(0.f);  // DiffuseAreaLight::L, one-sided
     if (pdfPos == 0 || pdfDir == 0 || Le.IsBlack()) return;
     Spectrum beta = (AbsDot(nLight, ray.d) * Le) / (lightPdf * pdfPos * pdfDir);
     if (beta.IsBlack()) return;
     TraceRecursive(ray, 0, beta, sampler, sc, MaxDepth, BeamRadius, out);
 }
 
+int g_ora_libm = 0;
+
 }  // namespace orp
+
+extern "C" {
+
+// 1: transcendentals from the host libm (as the reference) instead of include/bre_fmath.h
+void ora_set_libm(int on) { orp::g_ora_libm = on != 0; }
+
+}  // extern "C"
 
 extern "C" {
 

@@ -26,6 +26,23 @@ static const Float MaxFloat = 3.402823466e+38f;
 
 static inline Float gamma(int n) { return (n * MachineEpsilon) / (1 - n * MachineEpsilon); }
 
+// Transcendentals.  By default the oracle uses the same restatements as the GPU
+// (include/bre_fmath.h, within 2 ulp of libm) so photon and camera paths agree bit for bit; with
+// ora_set_libm(1) it calls the host libm (std::exp / std::log / std::sin / std::cos) as the
+// reference does (spectrum.h:222-224, homogeneous.cpp:47, grid.cpp:76,104, sampling.cpp:127) --
+// used to measure what that substitution changes in the image (tests/test_faithful.py).
+extern int g_ora_libm;
+static inline Float ora_exp(Float x) { return g_ora_libm ? std::exp(x) : bre_expf(x); }
+static inline Float ora_log(Float x) { return g_ora_libm ? std::log(x) : bre_logf(x); }
+static inline void ora_sincos(Float x, Float *s, Float *c) {
+    if (g_ora_libm) {
+        *s = std::sin(x);
+        *c = std::cos(x);
+    } else {
+        bre_sincosf(x, s, c);
+    }
+}
+
 // ---- RNG (rng.h:60-144) ----
 struct RNG {
     uint64_t state, inc;
@@ -156,7 +173,7 @@ struct Spectrum {
 };
 static inline Spectrum operator*(Float a, const Spectrum &s) { return s * a; }
 static inline Spectrum Exp(const Spectrum &s) {
-    return Spectrum(bre_expf(s.c[0]), bre_expf(s.c[1]), bre_expf(s.c[2]));
+    return Spectrum(ora_exp(s.c[0]), ora_exp(s.c[1]), ora_exp(s.c[2]));
 }
 
 // ---- sampling (sampling.cpp:113-133, sampling.h:159-165) ----
@@ -176,7 +193,7 @@ static inline void ConcentricSampleDisk(Float ux, Float uy, Float *dx, Float *dy
         theta = PiOver2 - PiOver4 * (ox / oy);
     }
     Float s, c;
-    bre_sincosf(theta, &s, &c);
+    ora_sincos(theta, &s, &c);
     *dx = c * r;
     *dy = s * r;
 }
@@ -205,7 +222,7 @@ static inline Float HG_Sample_p(Float g, const V3 &wo, V3 *wi, Float u0, Float u
     V3 v1, v2;
     CoordinateSystem(wo, &v1, &v2);
     Float sp, cp;
-    bre_sincosf(phi, &sp, &cp);
+    ora_sincos(phi, &sp, &cp);
     *wi = sinTheta * cp * v1 + sinTheta * sp * v2 + cosTheta * (-wo);
     return PhaseHG(-cosTheta, g);
 }
@@ -218,16 +235,23 @@ struct Ray {
     V3 operator()(Float t) const { return o + d * t; }
 };
 
-struct Quad {
-    V3 p0, e1, e2, n, ss, ts;
-    Float inv_e1sq, inv_e2sq, area;
-    Spectrum kd;
+// One pbrt Triangle (src/shapes/triangle.cpp) with the per-shape constants the passes use.
+struct Tri {
+    V3 p0, p1, p2;
+    V3 n;       // Intersect's normal: Normalize(Cross(dp02, dp12)), negated if flip (:292-297)
+    V3 ss, ts;  // BSDF frame: ss = Normalize(dpdu), ts = Cross(ns, ss) (reflection.h BSDF ctor)
+    V3 nS;      // Sample's normal: Normalize(Cross(p1 - p0, p2 - p0)), negated if flip (:552-560)
+    Float area;  // 0.5 * Cross(p1 - p0, p2 - p0).Length() (:535-541)
+    Spectrum kd, Le;
+    bool emit;
 };
 
 struct Scene {
-    std::vector<Quad> quads;
-    int light;
-    Spectrum Lemit;
+    std::vector<Tri> tris;
+    std::vector<int> lights;  // scene.lights: the emitting triangles, in triangle order
+    // ComputeLightPowerDistribution (integrator.cpp:217-225) -> Distribution1D (sampling.h:55-100)
+    std::vector<Float> lfunc, lcdf;
+    Float lfuncInt = 0;
     bool medium;
     Spectrum sigma_t, sigma_s;
     Float g;
@@ -239,26 +263,65 @@ struct Scene {
     Float gridSigmaT = 0, invMaxDensity = 0;
 };
 
+// Distribution1D::SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389)
+static int SampleDiscrete(const Scene &sc, Float u, Float *pdf) {
+    const int size = (int)sc.lcdf.size();
+    int first = 0, len = size;
+    while (len > 0) {
+        int half = len >> 1, middle = first + half;
+        if (sc.lcdf[middle] <= u) {
+            first = middle + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    const int offset = std::min(std::max(first - 1, 0), size - 2);  // Clamp(first - 1, 0, size - 2)
+    if (pdf) *pdf = (sc.lfuncInt > 0) ? sc.lfunc[offset] / (sc.lfuncInt * (Float)sc.lfunc.size()) : 0;
+    return offset;
+}
+
 static Scene make_scene(const bre_scene *s) {
     Scene sc;
-    for (int i = 0; i < s->n_quads; ++i) {
-        const bre_quad &q = s->quads[i];
-        Quad Q;
-        Q.p0 = V3(q.p0);
-        Q.e1 = V3(q.e1);
-        Q.e2 = V3(q.e2);
-        V3 c = Cross(Q.e1, Q.e2);
-        Q.area = c.Length();
-        Q.n = Normalize(c);
-        Q.ss = Normalize(Q.e1);
-        Q.ts = Cross(Q.n, Q.ss);
-        Q.inv_e1sq = 1 / Dot(Q.e1, Q.e1);
-        Q.inv_e2sq = 1 / Dot(Q.e2, Q.e2);
-        Q.kd = Spectrum(q.kd);
-        sc.quads.push_back(Q);
+    for (int i = 0; i < s->n_triangles; ++i) {
+        const bre_triangle &t = s->triangles[i];
+        Tri T;
+        T.p0 = V3(t.p[0]);
+        T.p1 = V3(t.p[1]);
+        T.p2 = V3(t.p[2]);
+        const V3 dp02 = T.p0 - T.p2, dp12 = T.p1 - T.p2;
+        // dpdu for uvs (0,0), (1,0), (1,1): (duv12[1] * dp02 - duv02[1] * dp12) * invdet, with
+        // duv12[1] = duv02[1] = -1 and invdet = 1 (triangle.cpp:276-285)
+        const V3 dpdu = (dp02 * (Float)-1 - dp12 * (Float)-1) * (Float)1;
+        T.n = Normalize(Cross(dp02, dp12));
+        T.nS = Normalize(Cross(T.p1 - T.p0, T.p2 - T.p0));
+        if (t.flip) {
+            T.n = -T.n;
+            T.nS = -T.nS;
+        }
+        T.ss = Normalize(dpdu);
+        T.ts = Cross(T.n, T.ss);
+        T.area = (Float)(0.5 * (double)Cross(T.p1 - T.p0, T.p2 - T.p0).Length());
+        T.kd = Spectrum(t.kd);
+        T.Le = Spectrum(t.Le);
+        T.emit = t.emit != 0;
+        if (T.emit) sc.lights.push_back(i);
+        sc.tris.push_back(T);
     }
-    sc.light = s->light_quad;
-    sc.Lemit = Spectrum(s->light_L);
+    // DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:53-55), .y()
+    const int n = (int)sc.lights.size();
+    for (int l : sc.lights) {
+        const Tri &T = sc.tris[l];
+        sc.lfunc.push_back(((T.Le * (Float)1) * T.area * Pi).y());
+    }
+    sc.lcdf.assign(n + 1, 0.f);
+    for (int i = 1; i < n + 1; ++i) sc.lcdf[i] = sc.lcdf[i - 1] + sc.lfunc[i - 1] / (Float)n;
+    sc.lfuncInt = sc.lcdf[n];
+    if (sc.lfuncInt == 0) {
+        for (int i = 1; i < n + 1; ++i) sc.lcdf[i] = Float(i) / Float(n);
+    } else {
+        for (int i = 1; i < n + 1; ++i) sc.lcdf[i] /= sc.lfuncInt;
+    }
     sc.medium = s->has_medium != 0;
     Spectrum sa(s->sigma_a);
     sc.sigma_s = Spectrum(s->sigma_s);
@@ -282,42 +345,116 @@ static Scene make_scene(const bre_scene *s) {
 
 struct Isect {
     V3 p, pError, n;
-    int quad;
+    int tri;
 };
 
-// Closest hit over all quads (strict <, so the lowest index wins a tie); sets ray.tMax like
-// GeometricPrimitive::Intersect (primitive.cpp:97-101).
-// One quad: plane solve, (u, v) in [0,1]^2, t in (0, ray.tMax); the hit point is rebuilt on the
-// quad with the parallelogram form of the triangle error bound.
-static bool IntersectQuad(const Quad &q, const Ray &ray, Float *tHit, Isect *isect) {
-    Float denom = Dot(q.n, ray.d);
-    if (denom == 0) return false;
-    Float t = Dot(q.n, q.p0 - ray.o) / denom;
-    if (!(t > 0 && t < ray.tMax)) return false;
-    V3 rel = ray(t) - q.p0;
-    Float u = Dot(rel, q.e1) * q.inv_e1sq;
-    Float v = Dot(rel, q.e2) * q.inv_e2sq;
-    if (!(u >= 0 && u <= 1 && v >= 0 && v <= 1)) return false;
+static inline int MaxDimension(const V3 &v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
+static inline V3 Permute(const V3 &v, int x, int y, int z) { return V3(v[x], v[y], v[z]); }
+static inline Float MaxComponent(const V3 &v) { return std::max(v.x, std::max(v.y, v.z)); }
+
+// Triangle::Intersect, triangle.cpp:177-300 (watertight ray-triangle test; no alpha texture)
+static bool IntersectTri(const Tri &T, const Ray &ray, Float *tHit, Isect *isect) {
+    const V3 &p0 = T.p0, &p1 = T.p1, &p2 = T.p2;
+    V3 p0t = p0 - ray.o, p1t = p1 - ray.o, p2t = p2 - ray.o;
+    int kz = MaxDimension(Abs(ray.d));
+    int kx = kz + 1;
+    if (kx == 3) kx = 0;
+    int ky = kx + 1;
+    if (ky == 3) ky = 0;
+    V3 d = Permute(ray.d, kx, ky, kz);
+    p0t = Permute(p0t, kx, ky, kz);
+    p1t = Permute(p1t, kx, ky, kz);
+    p2t = Permute(p2t, kx, ky, kz);
+    Float Sx = -d.x / d.z;
+    Float Sy = -d.y / d.z;
+    Float Sz = 1.f / d.z;
+    p0t.x += Sx * p0t.z;
+    p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z;
+    p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z;
+    p2t.y += Sy * p2t.z;
+    Float e0 = p1t.x * p2t.y - p1t.y * p2t.x;
+    Float e1 = p2t.x * p0t.y - p2t.y * p0t.x;
+    Float e2 = p0t.x * p1t.y - p0t.y * p1t.x;
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double p2txp1ty = (double)p2t.x * (double)p1t.y;
+        double p2typ1tx = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(p2typ1tx - p2txp1ty);
+        double p0txp2ty = (double)p0t.x * (double)p2t.y;
+        double p0typ2tx = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(p0typ2tx - p0txp2ty);
+        double p1txp0ty = (double)p1t.x * (double)p0t.y;
+        double p1typ0tx = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(p1typ0tx - p1txp0ty);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    Float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz;
+    p1t.z *= Sz;
+    p2t.z *= Sz;
+    Float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < ray.tMax * det)) return false;
+    else if (det > 0 && (tScaled <= 0 || tScaled > ray.tMax * det)) return false;
+    Float invDet = 1 / det;
+    Float b0 = e0 * invDet;
+    Float b1 = e1 * invDet;
+    Float b2 = e2 * invDet;
+    Float t = tScaled * invDet;
+    Float maxZt = MaxComponent(Abs(V3(p0t.z, p1t.z, p2t.z)));
+    Float deltaZ = gamma(3) * maxZt;
+    Float maxXt = MaxComponent(Abs(V3(p0t.x, p1t.x, p2t.x)));
+    Float maxYt = MaxComponent(Abs(V3(p0t.y, p1t.y, p2t.y)));
+    Float deltaX = gamma(5) * (maxXt + maxZt);
+    Float deltaY = gamma(5) * (maxYt + maxZt);
+    Float deltaE = 2 * (gamma(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    Float maxE = MaxComponent(Abs(V3(e0, e1, e2)));
+    Float deltaT = 3 * (gamma(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * std::abs(invDet);
+    if (t <= deltaT) return false;
+    Float xAbsSum = (std::abs(b0 * p0.x) + std::abs(b1 * p1.x) + std::abs(b2 * p2.x));
+    Float yAbsSum = (std::abs(b0 * p0.y) + std::abs(b1 * p1.y) + std::abs(b2 * p2.y));
+    Float zAbsSum = (std::abs(b0 * p0.z) + std::abs(b1 * p1.z) + std::abs(b2 * p2.z));
+    isect->pError = V3(xAbsSum, yAbsSum, zAbsSum) * gamma(7);
+    isect->p = p0 * b0 + p1 * b1 + p2 * b2;
+    isect->n = T.n;
     *tHit = t;
-    V3 ue1 = q.e1 * u, ve2 = q.e2 * v;
-    isect->p = q.p0 + ue1 + ve2;
-    isect->pError = (Abs(q.p0) + Abs(ue1) + Abs(ve2)) * gamma(6);
-    isect->n = q.n;
     return true;
 }
 
+// Scene::Intersect over the triangles in order (GeometricPrimitive::Intersect sets ray.tMax to the
+// hit, primitive.cpp:97-101; the reference's BVH order decides only exact ties, where the later
+// triangle of equal t wins here).
 static bool Intersect(const Scene &sc, Ray &ray, Isect *isect) {
     bool hit = false;
-    for (int i = 0; i < (int)sc.quads.size(); ++i) {
+    for (int i = 0; i < (int)sc.tris.size(); ++i) {
         Float t;
         Isect tmp;
-        if (!IntersectQuad(sc.quads[i], ray, &t, &tmp)) continue;
+        if (!IntersectTri(sc.tris[i], ray, &t, &tmp)) continue;
         ray.tMax = t;
         *isect = tmp;
-        isect->quad = i;
+        isect->tri = i;
         hit = true;
     }
     return hit;
+}
+
+// Triangle::Sample(u, pdf) (triangle.cpp:543-568) with UniformSampleTriangle (sampling.cpp)
+struct ShapeSample {
+    V3 p, pError, n;
+    Float pdf;
+};
+static ShapeSample SampleTri(const Tri &T, Float u0, Float u1) {
+    ShapeSample r;
+    const Float su0 = std::sqrt(u0);
+    const Float b0 = 1 - su0, b1 = u1 * su0;
+    const Float b2 = 1 - b0 - b1;
+    r.p = T.p0 * b0 + T.p1 * b1 + T.p2 * b2;
+    r.n = T.nS;
+    const V3 pAbsSum = Abs(T.p0 * b0) + Abs(T.p1 * b1) + Abs(T.p2 * b2);
+    r.pError = pAbsSum * gamma(6);
+    r.pdf = 1 / T.area;
+    return r;
 }
 
 // HomogeneousMedium (homogeneous.cpp:44-77)
@@ -329,7 +466,7 @@ static Spectrum HomogeneousTr(const Scene &sc, const Ray &ray) {
 template <class S>
 static bool HomogeneousSample(const Scene &sc, const Ray &ray, S &sampler, Float *tOut) {
     int channel = std::min((int)(sampler.Get1D() * 3), 3 - 1);
-    Float dist = -bre_logf(1 - sampler.Get1D()) / sc.sigma_t.c[channel];
+    Float dist = -ora_log(1 - sampler.Get1D()) / sc.sigma_t.c[channel];
     Float t = std::min(dist * ray.d.Length(), ray.tMax);
     *tOut = t;
     return t < ray.tMax;
@@ -414,7 +551,7 @@ static bool GridSample(const Scene &sc, const Ray &rWorld, S &sampler, Float *tO
     if (!UnitBoxIntersectP(ray, &tMin, &tMax)) return false;
     Float t = tMin;
     while (true) {
-        t -= bre_logf(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
+        t -= ora_log(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
         if (t >= tMax) break;
         if (GridDensity(sc, ray(t)) * sc.invMaxDensity > sampler.Get1D()) {
             *tOut = t;
@@ -431,7 +568,7 @@ static Spectrum GridTr(const Scene &sc, const Ray &rWorld, S &sampler) {
     if (!UnitBoxIntersectP(ray, &tMin, &tMax)) return Spectrum(1.f);
     Float Tr = 1, t = tMin;
     while (true) {
-        t -= bre_logf(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
+        t -= ora_log(1 - sampler.Get1D()) * sc.invMaxDensity / sc.gridSigmaT;
         if (t >= tMax) break;
         Float density = GridDensity(sc, ray(t));
         Tr *= 1 - std::max((Float)0, density * sc.invMaxDensity);

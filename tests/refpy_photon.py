@@ -280,20 +280,48 @@ def hg_sample(g, wo, u0, u1):
     return add(add(mul(v1, f32(sin_t * cp)), mul(v2, f32(sin_t * sp))), mul(tuple(-x for x in wo), cos_t))
 
 
+def _gam(n):
+    return gamma(n)
+
+
 class Scene:
     def __init__(self, s):
-        self.quads = []
-        for i in range(s.n_quads):
-            q = s.quads[i]
-            p0, e1, e2 = (tuple(f32(x) for x in v) for v in (q.p0, q.e1, q.e2))
-            c = cross(e1, e2)
-            n = normalize(c)
-            ss = normalize(e1)
-            self.quads.append(dict(p0=p0, e1=e1, e2=e2, n=n, ss=ss, ts=cross(n, ss), area=length(c),
-                                   ie1=f32(f32(1) / dot(e1, e1)), ie2=f32(f32(1) / dot(e2, e2)),
-                                   kd=tuple(f32(x) for x in q.kd)))
-        self.light = s.light_quad
-        self.Le = tuple(f32(x) for x in s.light_L)
+        # one dict per pbrt Triangle (shapes/triangle.cpp)
+        self.tris = []
+        self.lights = []
+        for i in range(s.n_triangles):
+            t = s.triangles[i]
+            p0, p1, p2 = (tuple(f32(x) for x in t.p[k]) for k in range(3))
+            dp02, dp12 = sub(p0, p2), sub(p1, p2)
+            # dpdu = (duv12[1] * dp02 - duv02[1] * dp12) * invdet with -1, -1, 1 (triangle.cpp:276-285)
+            dpdu = mul(sub(mul(dp02, f32(-1)), mul(dp12, f32(-1))), f32(1))
+            n = normalize(cross(dp02, dp12))
+            ns = normalize(cross(sub(p1, p0), sub(p2, p0)))
+            if t.flip:
+                n = tuple(-x for x in n)
+                ns = tuple(-x for x in ns)
+            ss = normalize(dpdu)
+            area = f32(0.5 * float(length(cross(sub(p1, p0), sub(p2, p0)))))
+            self.tris.append(dict(p=(p0, p1, p2), n=n, ns=ns, ss=ss, ts=cross(n, ss), area=area,
+                                  kd=tuple(f32(x) for x in t.kd), Le=tuple(f32(x) for x in t.Le)))
+            if t.emit:
+                self.lights.append(i)
+        # ComputeLightPowerDistribution: Power() = 1 * Lemit * area * Pi, its y() (diffuse.cpp:64-66)
+        func = []
+        for li in self.lights:
+            T = self.tris[li]
+            pw = tuple(f32(f32(f32(c * f32(1)) * T["area"]) * PI) for c in T["Le"])
+            func.append(f32(f32(f32(f32(0.212671) * pw[0]) + f32(f32(0.715160) * pw[1])) + f32(f32(0.072169) * pw[2])))
+        nl = len(func)
+        cdf = [f32(0)] * (nl + 1)
+        for i in range(1, nl + 1):
+            cdf[i] = f32(cdf[i - 1] + f32(func[i - 1] / f32(nl)))
+        fint = cdf[nl]
+        if fint == 0:
+            cdf = [f32(f32(i) / f32(nl)) for i in range(nl + 1)]
+        else:
+            cdf = [cdf[0]] + [f32(c / fint) for c in cdf[1:]]
+        self.lfunc, self.lcdf, self.lint = func, cdf, fint
         self.medium = bool(s.has_medium)
         self.sigma_t = tuple(f32(f32(a) + f32(b)) for a, b in zip(s.sigma_a, s.sigma_s))
         self.g = f32(s.g)
@@ -309,27 +337,101 @@ class Scene:
                 mx = v if mx < v else mx
             self.inv_max = f32(f32(1) / mx)
 
+    def sample_light(self, u):
+        """Distribution1D::SampleDiscrete (sampling.h:90-100) with FindInterval (pbrt.h:377-389)."""
+        size = len(self.lcdf)
+        first, ln = 0, size
+        while ln > 0:
+            half = ln >> 1
+            mid = first + half
+            if self.lcdf[mid] <= u:
+                first = mid + 1
+                ln -= half + 1
+            else:
+                ln = half
+        off = min(max(first - 1, 0), size - 2)
+        pdf = f32(self.lfunc[off] / f32(self.lint * f32(len(self.lfunc)))) if self.lint > 0 else f32(0)
+        return off, pdf
+
+    @staticmethod
+    def hit_tri(T, o, d, tmax):
+        """Triangle::Intersect (triangle.cpp:177-300): watertight test; (t, p, pError) or None."""
+        p0, p1, p2 = T["p"]
+        ad = vabs(d)
+        kz = (0 if ad[0] > ad[2] else 2) if ad[0] > ad[1] else (1 if ad[1] > ad[2] else 2)
+        kx = 0 if kz + 1 == 3 else kz + 1
+        ky = 0 if kx + 1 == 3 else kx + 1
+
+        def perm(v):
+            return [v[kx], v[ky], v[kz]]
+
+        dd = perm(d)
+        a, b, c = perm(sub(p0, o)), perm(sub(p1, o)), perm(sub(p2, o))
+        sx = f32(-dd[0] / dd[2])
+        sy = f32(-dd[1] / dd[2])
+        sz = f32(f32(1) / dd[2])
+        for v in (a, b, c):
+            v[0] = f32(v[0] + f32(sx * v[2]))
+            v[1] = f32(v[1] + f32(sy * v[2]))
+        e0 = f32(f32(b[0] * c[1]) - f32(b[1] * c[0]))
+        e1 = f32(f32(c[0] * a[1]) - f32(c[1] * a[0]))
+        e2 = f32(f32(a[0] * b[1]) - f32(a[1] * b[0]))
+        if e0 == 0 or e1 == 0 or e2 == 0:
+            e0 = f32(float(c[1]) * float(b[0]) - float(c[0]) * float(b[1]))
+            e1 = f32(float(a[1]) * float(c[0]) - float(a[0]) * float(c[1]))
+            e2 = f32(float(b[1]) * float(a[0]) - float(b[0]) * float(a[1]))
+        if (e0 < 0 or e1 < 0 or e2 < 0) and (e0 > 0 or e1 > 0 or e2 > 0):
+            return None
+        det = f32(f32(e0 + e1) + e2)
+        if det == 0:
+            return None
+        for v in (a, b, c):
+            v[2] = f32(v[2] * sz)
+        ts = f32(f32(f32(e0 * a[2]) + f32(e1 * b[2])) + f32(e2 * c[2]))
+        if det < 0 and (ts >= 0 or ts < f32(tmax * det)):
+            return None
+        if det > 0 and (ts <= 0 or ts > f32(tmax * det)):
+            return None
+        inv = f32(f32(1) / det)
+        b0, b1, b2 = f32(e0 * inv), f32(e1 * inv), f32(e2 * inv)
+        t = f32(ts * inv)
+        mz = max(abs(a[2]), max(abs(b[2]), abs(c[2])))
+        mx = max(abs(a[0]), max(abs(b[0]), abs(c[0])))
+        my = max(abs(a[1]), max(abs(b[1]), abs(c[1])))
+        dz = f32(_gam(3) * mz)
+        dx = f32(_gam(5) * f32(mx + mz))
+        dy = f32(_gam(5) * f32(my + mz))
+        de = f32(f32(2) * f32(f32(f32(f32(_gam(2) * mx) * my) + f32(dy * mx)) + f32(dx * my)))
+        me = max(abs(e0), max(abs(e1), abs(e2)))
+        dt = f32(f32(f32(3) * f32(f32(f32(f32(_gam(3) * me) * mz) + f32(de * mz)) + f32(dz * me))) * abs(inv))
+        if t <= dt:
+            return None
+        sums = [f32(f32(abs(f32(b0 * p0[k])) + abs(f32(b1 * p1[k]))) + abs(f32(b2 * p2[k]))) for k in range(3)]
+        perr = mul(tuple(sums), _gam(7))
+        p = add(add(mul(p0, b0), mul(p1, b1)), mul(p2, b2))
+        return t, p, perr
+
     def intersect(self, o, d):
         best = None
         tmax = INF
-        for i, q in enumerate(self.quads):
-            den = dot(q["n"], d)
-            if den == 0:
+        for i, T in enumerate(self.tris):
+            h = self.hit_tri(T, o, d, tmax)
+            if h is None:
                 continue
-            t = f32(dot(q["n"], sub(q["p0"], o)) / den)
-            if not (t > 0 and t < tmax):
-                continue
-            rel = sub(add(o, mul(d, t)), q["p0"])
-            u = f32(dot(rel, q["e1"]) * q["ie1"])
-            v = f32(dot(rel, q["e2"]) * q["ie2"])
-            if not (0 <= u <= 1 and 0 <= v <= 1):
-                continue
-            tmax = t
-            ue1, ve2 = mul(q["e1"], u), mul(q["e2"], v)
-            p = add(add(q["p0"], ue1), ve2)
-            perr = mul(add(add(vabs(q["p0"]), vabs(ue1)), vabs(ve2)), gamma(6))
-            best = (p, perr, i)
+            tmax = h[0]
+            best = (h[1], h[2], i)
         return best, tmax
+
+    def sample_tri(self, T, u0, u1):
+        """Triangle::Sample (triangle.cpp:543-568): point, pError, normal, area pdf."""
+        su0 = f32(np.sqrt(u0))
+        b0, b1 = f32(f32(1) - su0), f32(u1 * su0)
+        b2 = f32(f32(f32(1) - b0) - b1)
+        p0, p1, p2 = T["p"]
+        a, b, c = mul(p0, b0), mul(p1, b1), mul(p2, b2)
+        p = add(add(a, b), c)
+        perr = mul(add(add(vabs(a), vabs(b)), vabs(c)), _gam(6))
+        return p, perr, T["ns"], f32(f32(1) / T["area"])
 
     def tr(self, d, tmax):
         x = f32(tmax * length(d))
@@ -439,25 +541,22 @@ def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
     """Beams of one photon, in the reference's push order: list of (start, end, radius, power)."""
     rng = RNG(seq)
     out = []
-    rng.uniform()  # light choice (one light)
+    ln, light_pdf = sc.sample_light(rng.uniform())  # lightDistr->SampleDiscrete
     u0 = rng.get2d()
     u1 = rng.get2d()
     rng.uniform()  # time
-    L = sc.quads[sc.light]
-    ue1, ve2 = mul(L["e1"], u0[0]), mul(L["e2"], u0[1])
-    p = add(add(L["p0"], ue1), ve2)
-    perr = mul(add(add(vabs(L["p0"]), vabs(ue1)), vabs(ve2)), gamma(6))
-    pdf_pos = f32(f32(1) / L["area"])
+    L = sc.tris[sc.lights[ln]]
+    p, perr, nl, pdf_pos = sc.sample_tri(L, *u0)
     wl = cosine_hemisphere(*u1)
     pdf_dir = f32(wl[2] * INV_PI)
-    v1, v2 = coordinate_system(L["n"])
-    w = add(add(mul(v1, wl[0]), mul(v2, wl[1])), mul(L["n"], wl[2]))
-    o = offset_origin(p, perr, L["n"], w)
-    Le = sc.Le if dot(L["n"], w) > 0 else (f32(0),) * 3
+    v1, v2 = coordinate_system(nl)
+    w = add(add(mul(v1, wl[0]), mul(v2, wl[1])), mul(nl, wl[2]))
+    o = offset_origin(p, perr, nl, w)
+    Le = L["Le"] if dot(nl, w) > 0 else (f32(0),) * 3
     if pdf_pos == 0 or pdf_dir == 0 or all(x == 0 for x in Le):
         return out
-    ad = f32(abs(dot(L["n"], w)))
-    den = f32(f32(f32(1) * pdf_pos) * pdf_dir)
+    ad = f32(abs(dot(nl, w)))
+    den = f32(f32(light_pdf * pdf_pos) * pdf_dir)
     beta = tuple(f32(f32(ad * x) / den) for x in Le)
     if all(x == 0 for x in beta):
         return out
@@ -489,7 +588,7 @@ def trace_photon(sc: Scene, seq: int, max_depth: int, radius: float):
             else:
                 bm = sc.tr(d, tmax) if sc.medium else (f32(1),) * 3
             out.append((o, hit[0], f32(radius), tuple(f32(a * b) for a, b in zip(bm, beta))))
-            q = sc.quads[hit[2]]
+            q = sc.tris[hit[2]]
             ux, uy = rng.get2d()
             if all(x == 0 for x in q["kd"]):
                 return

@@ -48,9 +48,15 @@ def world(body, medium='MakeNamedMedium "fog" "string type" "homogeneous" "rgb s
     return HEAD + "WorldBegin\n" + medium + body + "WorldEnd\n"
 
 
-def quads(s):
-    return np.array([[list(getattr(s.quads[i], f)) for f in ("p0", "e1", "e2", "kd")] for i in range(s.n_quads)],
-                    np.float32)
+def tris(s):
+    """(n, 5, 3): the three world-space vertices, kd and Le of every triangle."""
+    T = s.triangles
+    return np.array([[list(T[i].p[0]), list(T[i].p[1]), list(T[i].p[2]), list(T[i].kd), list(T[i].Le)]
+                     for i in range(s.n_triangles)], np.float32)
+
+
+def tri_flags(s):
+    return [(s.triangles[i].emit, s.triangles[i].flip) for i in range(s.n_triangles)]
 
 
 def test_host_library_exports_every_declared_symbol(pb):
@@ -67,12 +73,11 @@ def test_c2_scene_file_is_the_benchmark_scene(pb, sc):
     s = pb.parse_file(os.path.join(SCENES, "cornell_fog_c2.pbrt"))
     assert s.ok and s.n_errors == 0 and s.n_warnings == 0, s.messages
     ref = sc.cornell_scene(0.05, 0.5, 0.0)
-    # every field but the light's edges is bit-identical; 0.65f - 0.35f is one ulp below 0.3f
-    a, b = quads(s.scene), quads(ref)
-    assert s.scene.n_quads == ref.n_quads == 7 and s.scene.light_quad == ref.light_quad
-    assert np.array_equal(a[:6], b[:6])
-    assert np.allclose(a[6], b[6], rtol=0, atol=1e-7)
-    for f in ("light_L", "sigma_a", "sigma_s", "cam_pos", "cam_look", "cam_up"):
+    # 7 two-triangle meshes, vertices bit-identical (identity CTM), the light mesh emitting
+    assert s.scene.n_triangles == ref.n_triangles == 14
+    assert np.array_equal(tris(s.scene), tris(ref))
+    assert tri_flags(s.scene) == tri_flags(ref) == [(0, 0)] * 12 + [(1, 0)] * 2
+    for f in ("sigma_a", "sigma_s", "cam_pos", "cam_look", "cam_up"):
         assert list(getattr(s.scene, f)) == list(getattr(ref, f)), f
     assert s.scene.has_medium == 1 and s.scene.g == 0.0 and s.scene.cam_fov_deg == 60.0
     p = s.params
@@ -152,20 +157,25 @@ def test_transforms_apply_to_shape_vertices(pb):
     body = LIGHT + 'AttributeBegin\nTranslate 0 0.5 0\nRotate 90 0 0 1\nScale 0.5 0.5 0.5\n' + FLOOR + 'AttributeEnd\n'
     s = pb.parse_string(world(body))
     assert s.ok, s.messages
-    q = quads(s.scene)[1]
-    # floor vertices (0,0,0) (0,0,1) (1,0,0) through T * R(90 about z) * S(0.5): x -> y
-    assert np.allclose(q[0], [0, 0.5, 0], atol=1e-7)
-    assert np.allclose(q[1], [0, 0, 0.5], atol=1e-7)
-    assert np.allclose(q[2], [0, 0.5, 0], atol=1e-7)  # cos(pi/2) in float is -4.4e-8, scaled by 0.5
+    q = tris(s.scene)
+    assert q.shape[0] == 4  # light (2 triangles), then the floor
+    # floor triangle (0,0,0) (0,0,1) (1,0,1) through T(0,.5,0) * R(90 about z) * S(0.5): x -> y
+    assert np.allclose(q[2, 0], [0, 0.5, 0], atol=1e-7)
+    assert np.allclose(q[2, 1], [0, 0.5, 0.5], atol=1e-7)
+    assert np.allclose(q[2, 2], [0, 1.0, 0.5], atol=1e-7)  # cos(pi/2) in float is -4.4e-8, scaled by 0.5
+    # a rotation keeps handedness: no flip; a mirror flips (Transform::SwapsHandedness)
+    assert tri_flags(s.scene)[2] == (0, 0)
+    m = pb.parse_string(world(LIGHT + 'AttributeBegin\nScale -1 1 1\n' + FLOOR + 'AttributeEnd\n'))
+    assert m.ok and tri_flags(m.scene)[2:] == [(0, 1), (0, 1)]
+    r = pb.parse_string(world(LIGHT + 'AttributeBegin\nReverseOrientation\n' + FLOOR + 'AttributeEnd\n'))
+    assert r.ok and tri_flags(r.scene)[2:] == [(0, 1), (0, 1)]
 
 
 def test_unsupported_statements_are_reported(pb):
     cases = {
         'Shape "sphere" "float radius" 1\n': 'Shape "sphere" is not supported',
-        'Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point P" [0 0 0 1 0 0 1.2 1 0 0 1 0]\n':
-            "not a parallelogram",
-        'Shape "trianglemesh" "integer indices" [0 1 2 0 3 2] "point P" [0 0 0 1 0 0 1 1 0 0 1 0]\n':
-            "do not share a diagonal",
+        'Shape "trianglemesh" "integer indices" [0 1 2 0 2] "point P" [0 0 0 1 0 0 1 1 0 0 1 0]\n':
+            "not a multiple of 3",
         'Shape "trianglemesh" "integer indices" [0 1 9 0 2 3] "point P" [0 0 0 1 0 0 1 1 0 0 1 0]\n':
             "out of-bounds vertex index 9",
         'LightSource "point" "rgb I" [1 1 1]\n': 'LightSource "point" is not supported',
@@ -187,8 +197,9 @@ def test_scenes_the_model_cannot_render_fail(pb):
     # walls with a non-transition "" "" interface inherit the ray's medium: fine
     s = pb.parse_string(world(LIGHT + 'AttributeBegin\nMediumInterface "" ""\n' + FLOOR + "AttributeEnd\n"))
     assert s.ok, s.messages
-    # two emitters / none
-    assert not pb.parse_string(world(LIGHT + LIGHT + FLOOR)).ok
+    # several emitting meshes are fine (one DiffuseAreaLight per triangle); none is not
+    two = pb.parse_string(world(LIGHT + LIGHT + FLOOR))
+    assert two.ok and [e for e, _ in tri_flags(two.scene)] == [1, 1, 1, 1, 0, 0]
     assert not pb.parse_string(world(FLOOR)).ok
     # a camera transform that is not one LookAt
     s = pb.parse_string("Scale -1 1 1\n" + world(LIGHT + FLOOR))

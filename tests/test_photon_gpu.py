@@ -54,7 +54,7 @@ def test_photon_pass_bit_exact(bre, oracle, scene_mod, cfg):
 
 
 def test_photon_pass_vacuum(bre, oracle, scene_mod):
-    s = scene_mod.make_scene(scene_mod.cornell_quads(), 6, (17.0, 12.0, 4.0))  # no medium
+    s = scene_mod.make_scene(scene_mod.cornell_meshes())  # no medium
     ref = oracle.trace_photons(s, 5000, max_depth=5)
     with bre.BeamGather(0) as g:
         g.trace_photons(s, 5000, max_depth=5)
@@ -75,7 +75,14 @@ def test_photon_pass_empty_and_errors(bre, scene_mod):
         with pytest.raises(bre.BreError):
             g.trace_photons(s, 10, max_depth=scene_mod.MAX_DEPTH + 1)
         bad = scene_mod.cornell_scene()
-        bad.light_quad = 9
+        bad.triangles[12].emit = bad.triangles[13].emit = 0  # no emitter
+        with pytest.raises(bre.BreError):
+            g.trace_photons(bad, 10)
+        bad = scene_mod.cornell_scene()
+        bad.n_triangles = 0
+        with pytest.raises(bre.BreError):
+            g.trace_photons(bad, 10)
+        bad.n_triangles = scene_mod.MAX_TRIANGLES + 1
         with pytest.raises(bre.BreError):
             g.trace_photons(bad, 10)
 

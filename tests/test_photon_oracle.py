@@ -202,7 +202,7 @@ def test_photon_pass_properties(oracle, scene_mod):
 
 
 def test_photon_pass_vacuum_and_depth(oracle, scene_mod):
-    vac = scene_mod.make_scene(scene_mod.cornell_quads(), 6, (17.0, 12.0, 4.0))
+    vac = scene_mod.make_scene(scene_mod.cornell_meshes())
     a = oracle.trace_photons(vac, 5000, max_depth=5)
     assert a["counts"].max() <= 5
     # vacuum: beam k+1 starts where beam k ended (up to the surface offset)
