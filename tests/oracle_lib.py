@@ -59,9 +59,15 @@ class Oracle:
         lib.ora_scrambled_radical_inverse.restype = F
         lib.ora_shuffle.argtypes = [U64, I32, P]
         lib.ora_grid_density.argtypes = [P, I64, P, P]
+        lib.ora_set_libm.argtypes = [I32]
         lib.ora_grid_eval.argtypes = [P, I32, I64, P, P, P, U64, P, P]
 
     # -- primitives --
+    def set_libm(self, on: bool):
+        """Reference-faithful transcendentals: std::exp / std::log / std::sin / std::cos (the host libm,
+        as pbrt calls them) instead of the Cephes restatement the GPU shares (include/bre_fmath.h)."""
+        self.lib.ora_set_libm(int(bool(on)))
+
     def slab_pad(self) -> float:
         return float(self.lib.ora_slab_pad())
 
