@@ -1,16 +1,111 @@
-// bre_gather_demo.cpp — C++ host program using the integrator mirror (photonbeam_gpu.h):
-// one iteration of "build beams -> record camera segments -> batched gather -> resolve image"
-// on a small deterministic scene, printing the image sum.  Exit code 0 on success.
+// bre_gather_demo.cpp — C++ host program using the integrator mirror (photonbeam_gpu.h) the way
+// adapters/pbrt/photonbeam.patch does: build the iteration's beams (PhotonBeamGpuBVH::Build,
+// photonbeam.cpp:438), record camera segments in per-thread SegmentRecorders (:494-508), one
+// Gather per recorder into the pixel Ld buffer, ResolveImage (:578).
+//
+//   bre_gather_demo [W]                      built-in lattice scene, prints the image sum
+//   bre_gather_demo --beams B --segments S --out O [--split K] [--iteration I]
+//       B: int64 n, then n x {start xyz, end xyz, radius, powerEnd rgb} float32
+//       S: int64 n, int64 nPixels, float32 R, then n x {o xyz, p xyz, d xyz, tMax} float32 + int32 pixel
+//       O: nPixels x rgb float32, the resolved image L = Ld / (I + 1)
+//       K: number of recorders the segments are dealt to round-robin (the patch's per-thread
+//          recorders), each gathered with its own call
+// Exit code 0 on success, 1 on a libbre or IO error, 2 without a GPU.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
 #include <vector>
 
 #include "photonbeam_gpu.h"
 
 using namespace bre_host;
 
-int main(int argc, char **argv) {
-    const int W = argc > 1 ? std::atoi(argv[1]) : 64, H = W;
+namespace {
+
+template <typename T>
+bool ReadAll(FILE *f, T *dst, size_t n) {
+    return std::fread(dst, sizeof(T), n, f) == n;
+}
+
+int FileMode(const char *beamsPath, const char *segPath, const char *outPath, int split, int iteration) {
+    FILE *fb = std::fopen(beamsPath, "rb");
+    FILE *fs = std::fopen(segPath, "rb");
+    if (!fb || !fs) {
+        std::fprintf(stderr, "bre_gather_demo: cannot open %s\n", !fb ? beamsPath : segPath);
+        return 1;
+    }
+    int64_t nb = 0, ns = 0, npix = 0;
+    float R = 0;
+    if (!ReadAll(fb, &nb, 1) || nb < 0 || !ReadAll(fs, &ns, 1) || !ReadAll(fs, &npix, 1) || !ReadAll(fs, &R, 1) ||
+        ns < 0 || npix <= 0) {
+        std::fprintf(stderr, "bre_gather_demo: bad header\n");
+        return 1;
+    }
+    std::vector<PhotonBeam> beams((size_t)nb);
+    for (auto &b : beams) {
+        float v[10];
+        if (!ReadAll(fb, v, 10)) {
+            std::fprintf(stderr, "bre_gather_demo: short beam file\n");
+            return 1;
+        }
+        b.start = {v[0], v[1], v[2]};
+        b.end = {v[3], v[4], v[5]};
+        b.radius = v[6];
+        b.powerEnd = {v[7], v[8], v[9]};
+    }
+    std::vector<SegmentRecorder> recorders((size_t)(split > 0 ? split : 1));
+    for (int64_t i = 0; i < ns; ++i) {
+        float v[10];
+        int32_t pixel;
+        if (!ReadAll(fs, v, 10) || !ReadAll(fs, &pixel, 1)) {
+            std::fprintf(stderr, "bre_gather_demo: short segment file\n");
+            return 1;
+        }
+        CameraSegment s;
+        s.o = {v[0], v[1], v[2]};
+        s.p = {v[3], v[4], v[5]};
+        s.d = {v[6], v[7], v[8]};
+        s.tMax = v[9];
+        s.pixel = pixel;
+        recorders[(size_t)(i % (int64_t)recorders.size())].Record(s);
+    }
+    std::fclose(fb);
+    std::fclose(fs);
+
+    PhotonBeamGpuBVH bvh(0);
+    if (!bvh.Ok()) {
+        std::fprintf(stderr, "no GPU: %s\n", bvh.LastError().c_str());
+        return 2;
+    }
+    if (!bvh.Build(beams)) {
+        std::fprintf(stderr, "build: %s\n", bvh.LastError().c_str());
+        return 1;
+    }
+    std::vector<float> ld(3 * (size_t)npix, 0.f);
+    for (const auto &r : recorders)
+        if (r.Size() && !bvh.Gather(r, R, ld)) {
+            std::fprintf(stderr, "gather: %s\n", bvh.LastError().c_str());
+            return 1;
+        }
+    std::vector<float> rgb;
+    ResolveImage(ld, iteration, rgb);
+    FILE *fo = std::fopen(outPath, "wb");
+    if (!fo || std::fwrite(rgb.data(), sizeof(float), rgb.size(), fo) != rgb.size()) {
+        std::fprintf(stderr, "bre_gather_demo: cannot write %s\n", outPath);
+        return 1;
+    }
+    std::fclose(fo);
+    bre_stats st;
+    if (bvh.Stats(&st))
+        std::printf("bre_gather_demo: %lld beams, %lld segments in %zu gathers, %lld nodes\n", (long long)nb,
+                    (long long)ns, recorders.size(), (long long)st.n_nodes);
+    return 0;
+}
+
+int LatticeMode(int W) {
+    const int H = W;
     PhotonBeamParams params;
     params.initialBeamRadius = 0.02f;
     std::vector<PhotonBeam> beams;
@@ -58,4 +153,33 @@ int main(int argc, char **argv) {
     for (float v : rgb) sum += v;
     std::printf("bre_gather_demo: %zu beams, %lld segments, image sum %.9g\n", beams.size(), (long long)rec.Size(), sum);
     return sum > 0 ? 0 : 1;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const char *beams = nullptr, *segs = nullptr, *out = nullptr;
+    int split = 1, iteration = 0;
+    for (int i = 1; i < argc; ++i) {
+        const bool more = i + 1 < argc;
+        if (!std::strcmp(argv[i], "--beams") && more) beams = argv[++i];
+        else if (!std::strcmp(argv[i], "--segments") && more) segs = argv[++i];
+        else if (!std::strcmp(argv[i], "--out") && more) out = argv[++i];
+        else if (!std::strcmp(argv[i], "--split") && more) split = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--iteration") && more) iteration = std::atoi(argv[++i]);
+        else if (argv[i][0] != '-' && !beams) return LatticeMode(std::atoi(argv[i]));
+        else {
+            std::fprintf(stderr, "usage: bre_gather_demo [W] | --beams B --segments S --out O [--split K] "
+                                 "[--iteration I]\n");
+            return 1;
+        }
+    }
+    if (beams || segs || out) {
+        if (!beams || !segs || !out) {
+            std::fprintf(stderr, "bre_gather_demo: --beams, --segments and --out go together\n");
+            return 1;
+        }
+        return FileMode(beams, segs, out, split, iteration);
+    }
+    return LatticeMode(64);
 }
