@@ -298,8 +298,8 @@ __device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, const ScanBea
     return (nn_lo >= 1e-2f) & (tn > (B.ab + S.al) * nl);
 }
 
-constexpr int kTileBlock = 256;  // 4 waves
-constexpr int kQueueCap = 128;   // >= 63 left over + 64 appended by one beam
+constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
+constexpr int kQueueCap = 256;   // >= 63 left over + 128 appended by one scan step (two beams)
 constexpr int kRing = 64;        // leaf-base ring: queue entries reference < 64 distinct leaves (see push)
 
 struct TileShared {
@@ -420,9 +420,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int cur_slot = -1;         // ring slot of the current leaf (-1: none yet)
     int64_t cur_first = 0;     // first beam of the current leaf
 
-    // queue the (beam, lane) survivors of beam j of the current leaf; drain 64 at a time.  A leaf
-    // takes a ring slot at its first push: the < 64 entries left after a drain reference < 64 slots,
-    // all among the last 63 assigned, so a kRing = 64 ring never reuses a slot a live entry holds.
+    // queue the (beam, lane) survivors of beam j of the current leaf.  A leaf takes a ring slot at
+    // its first push: the < 64 entries left after a drain reference < 64 slots, all among the last
+    // 63 assigned, so a kRing = 64 ring never reuses a slot a live entry holds (a scan step pushes
+    // two beams of one leaf, then drains).
     const auto push = [&](int j, bool need) {
         const unsigned long long m = __ballot(need);
         if (m == 0ull) return;
@@ -436,16 +437,19 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             sh.q[pos] = ((uint32_t)cur_slot << 12) | ((uint32_t)j << 6) | (uint32_t)lane;
         }
         t1 += __popcll(m);
+    };
+    // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan)
+    const auto drain = [&]() {
         __builtin_amdgcn_wave_barrier();
-        if (t1 - h1 >= 64) {
+        while (t1 - h1 >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
             if (BRE_ABLATE != 2) tile_exact(sh, h1, 64, srec, sd, seg0, recs, pw, R, count_c);
             h1 += 64;
-            if (h1 >= 1024) {
-                h1 -= 1024;
-                t1 -= 1024;
-            }
             __builtin_amdgcn_wave_barrier();
+        }
+        if (h1 >= 1024) {
+            h1 -= 1024;
+            t1 -= 1024;
         }
     };
 
@@ -497,15 +501,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 cand += hit;
                 pf.rejects += hit & !need;
                 push(j, need);
+                drain();
             }
             return;
         }
-        if (!prefilter) {
-            for (int j = 0; j < nb; ++j) push(j, lane_on);
-            return;
-        }
         // two kept beams per step: independent broadcasts and prefilters (ILP), then the survivors
-        // are queued beam by beam in order
+        // are queued beam by beam in order (without the prefilter every beam is kept, km = all, and
+        // every lane on the leaf's box queues it)
         unsigned long long todo = km;
         while (todo != 0ull) {
             const int j1 = __ffsll((long long)todo) - 1;
@@ -514,11 +516,12 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
             const ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);  // both beams' reads issued together
-            const bool f1 = scan_far(SL, L.au, B1), f2 = scan_far(SL, L.au, B2);
+            const bool f1 = prefilter && scan_far(SL, L.au, B1), f2 = prefilter && scan_far(SL, L.au, B2);
             const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
             const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
             push(j1, n1);
             if (two) push(j2, n2);
+            drain();
         }
     };
 
@@ -527,69 +530,86 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // the production instantiation re-reads the lane's o, tmax and 1/d from its SegRec at each
         // node visit instead of holding them in VGPRs through the leaf scans (register budget)
         const float4 *my = reinterpret_cast<const float4 *>(srec + (s < nseg ? s : nseg - 1));
-        if (root < 0) {
-            leaf(root, valid);
-        } else {
-            int node = root;
-            int sp = 0;
-            while (true) {
-                node = __builtin_amdgcn_readfirstlane(node);
-                const NodeV n = load_node(nodes, node);
-                if (COUNT) ++visits;
-                const int32_t c0 = n.c0, c1 = n.c1;
-                f3 lo = L.o, li = L.invs;
-                float lt = L.tmax;
-                if (!COUNT) {
-                    // an opaque copy of the address per visit: keeps the compiler from hoisting the
-                    // two loads out of the loop (and the 7 values back into registers)
-                    const float4 *mp = my;
-                    asm volatile("" : "+v"(mp));
-                    const float4 a0 = mp[0], a3 = mp[3];
-                    lo = mk(a0.x, a0.y, a0.z);
-                    lt = a0.w;
-                    li = mk(a3.x, a3.y, a3.z);
+        // Leaf children found at a node visit are scanned at the top of the next step, c0's before
+        // c1's, so the leaf scan (and the exact stage inside it) is inlined once.
+        int32_t lc0 = 0, lc1 = 0;
+        unsigned long long lm0 = 0ull, lm1 = 0ull;  // lanes on each pending leaf's box (0: none)
+        int node = root;
+        bool have_node = root >= 0;
+        if (!have_node) {
+            lc0 = root;
+            lm0 = __ballot(valid);
+        }
+        int sp = 0;
+        while (true) {
+#pragma nounroll
+            for (int i = 0; i < 2; ++i) {
+                const unsigned long long m = i ? lm1 : lm0;
+                if (m != 0ull) leaf(i ? lc1 : lc0, ((m >> lane) & 1ull) != 0ull);
+            }
+            lm0 = lm1 = 0ull;
+            if (!have_node) {
+                if (sp == 0) break;
+                --sp;
+                node = sh.stk[sp];
+            }
+            node = __builtin_amdgcn_readfirstlane(node);
+            const NodeV n = load_node(nodes, node);
+            if (COUNT) ++visits;
+            const int32_t c0 = n.c0, c1 = n.c1;
+            f3 lo = L.o, li = L.invs;
+            float lt = L.tmax;
+            if (!COUNT) {
+                // an opaque copy of the address per visit: keeps the compiler from hoisting the
+                // two loads out of the loop (and the 7 values back into registers)
+                const float4 *mp = my;
+                asm volatile("" : "+v"(mp));
+                const float4 a0 = mp[0], a3 = mp[3];
+                lo = mk(a0.x, a0.y, a0.z);
+                lt = a0.w;
+                li = mk(a3.x, a3.y, a3.z);
+            }
+            float te0 = 0.f, te1 = 0.f;
+            const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, lo, li, lt, te0);
+            const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, lo, li, lt, te1);
+            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+            bool go0 = m0 != 0ull, go1 = m1 != 0ull;
+            if (go0 && c0 < 0) {
+                lc0 = c0;
+                lm0 = m0;
+                go0 = false;
+            }
+            if (go1 && c1 < 0) {
+                lc1 = c1;
+                lm1 = m1;
+                go1 = false;
+            }
+            have_node = true;
+            if (go0 && go1) {
+                // near child first, judged by the first lane that enters both
+                const unsigned long long both = m0 & m1;
+                bool first0 = true;
+                if (both != 0ull) {
+                    const int fl = __ffsll((long long)both) - 1;
+                    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
+                    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
+                    first0 = !(b < a);
                 }
-                float te0 = 0.f, te1 = 0.f;
-                const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, lo, li, lt, te0);
-                const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, lo, li, lt, te1);
-                const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-                bool go0 = m0 != 0ull, go1 = m1 != 0ull;
-                if (go0 && c0 < 0) {
-                    leaf(c0, h0);
-                    go0 = false;
+                const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
+                if (sp >= stack_cap) {
+                    // never silent: the host turns the flag into BRE_ERR_STATE (bre_api.hip)
+                    if (lane == 0) atomicOr(&ctr->flags, kFlagStack);
+                    break;
                 }
-                if (go1 && c1 < 0) {
-                    leaf(c1, h1);
-                    go1 = false;
-                }
-                if (go0 && go1) {
-                    // near child first, judged by the first lane that enters both
-                    const unsigned long long both = m0 & m1;
-                    bool first0 = true;
-                    if (both != 0ull) {
-                        const int fl = __ffsll((long long)both) - 1;
-                        const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
-                        const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
-                        first0 = !(b < a);
-                    }
-                    const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
-                    if (sp >= stack_cap) {
-                        // never silent: the host turns the flag into BRE_ERR_STATE (bre_api.hip)
-                        if (lane == 0) atomicOr(&ctr->flags, kFlagStack);
-                        break;
-                    }
-                    sh.stk[sp] = far;
-                    ++sp;
-                    node = near;
-                } else if (go0) {
-                    node = c0;
-                } else if (go1) {
-                    node = c1;
-                } else {
-                    if (sp == 0) break;
-                    --sp;
-                    node = sh.stk[sp];
-                }
+                sh.stk[sp] = far;
+                ++sp;
+                node = near;
+            } else if (go0) {
+                node = c0;
+            } else if (go1) {
+                node = c1;
+            } else {
+                have_node = false;
             }
         }
         // drain the prefilter survivors
