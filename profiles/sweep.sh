@@ -1,8 +1,14 @@
-set -e
-mkdir -p gpurun_out/sweep8
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_camera_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/sweep8/pytest.log 2>&1
-for cfg in "--workload synthetic" "--workload c2"; do
-  tag=$(echo $cfg | tr -d ' -')
-  timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu $cfg --json-out gpurun_out/sweep8/$tag.json > gpurun_out/sweep8/$tag.log 2>&1
-  echo "$cfg done"
+#!/bin/bash
+# Bench sweep over argument sets (no CPU leg / PMC / counters pass); one JSON per set.
+# usage (repo root, via gpurun): profiles/sweep.sh OUTDIR "ARGS1" "ARGS2" ...
+set -o pipefail
+OUT=${1:-gpurun_out/sweep}
+shift || true
+mkdir -p "$OUT"
+i=0
+for a in "$@"; do
+  i=$((i + 1))
+  timeout -k 10 400 python -u bench.py --no-cpu --no-pmc --no-diag --json-out "$OUT/s$i.json" $a > "$OUT/s$i.log" 2>&1 \
+      || { echo "[$a] failed"; tail -n 20 "$OUT/s$i.log"; exit 1; }
+  python3 -c "import json;d=json.load(open('$OUT/s$i.json'));print('[$a]', round(d['value']), round(d['gather_kernel_ms'],1), [round(x) for x in d['gather_ms_per_step'][::3]])"
 done
