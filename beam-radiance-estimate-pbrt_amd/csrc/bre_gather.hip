@@ -41,6 +41,16 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
 #endif
+// BRE_PHASE_TIMING 1 (profiling builds only): the production tile kernel adds, per wave, the
+// shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
+// `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
+// whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
+#ifndef BRE_PHASE_TIMING
+#define BRE_PHASE_TIMING 0
+#endif
+__device__ __forceinline__ unsigned long long phase_clock() {
+    return BRE_PHASE_TIMING ? (unsigned long long)__builtin_amdgcn_s_memtime() : 0ull;
+}
 
 struct Prof {
     unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0;
@@ -326,16 +336,19 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const uint32_t e = sh.q[(first + (on ? lane : 0)) & (kQueueCap - 1)];  // FIFO ring
     const int sl = (int)(e & 63u);
     const int64_t b = (int64_t)sh.leaf[e >> 12] + ((e >> 6) & 63u);
-    // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
+    // every load of the pair is issued at once (one memory round trip per batch; most queued pairs
+    // pass the box test, so the second half is rarely wasted)
     const float4 *sr = reinterpret_cast<const float4 *>(srec + seg0 + sl);
     const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
     const float4 s0 = sr[0], s3 = sr[3], bx = rb[0], by = rb[1];
+    const float4 s1 = sr[1], s2 = sr[2], bz = rb[2], bw = rb[3];
+    const float4 pv = pw[b];  // off lanes (a partial batch) read entry `first`: a valid beam
+    // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
     const float tmax = s0.w;
     const Box6 box{bx.x, bx.y, bx.z, bx.w, by.x, by.y};
     float te;
     bool hit = on & node_test(box, o, mk(s3.x, s3.y, s3.z), tmax, te);
-    const float4 s2 = sr[2];
     const bool inf = s2.w != 0.f;  // has_inf (integer 1 as float bits: a denormal, never 0)
     if (__ballot(on & inf) != 0ull) {
         if (on & inf) {
@@ -347,9 +360,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
         }
     }
     if (__ballot(hit) == 0ull) return;
-    // phase 2: closest points + kernel (the power load is issued first: most box hits contribute)
-    const float4 pv = hit ? pw[b] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 bz = rb[2], bw = rb[3], s1 = sr[1];
+    // phase 2: closest points + kernel
     if (hit) {
         const float maxd = R + bw.y;  // MaxDistance = currentBeamRadius + beam->radius
         float dist;
@@ -422,6 +433,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int ring_next = 0;         // next leaf-base ring slot
     int cur_slot = -1;         // ring slot of the current leaf (-1: none yet)
     int64_t cur_first = 0;     // first beam of the current leaf
+    unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
+    const unsigned long long ph_t0 = phase_clock();
 
     // queue the (beam, lane) survivors of beam j of the current leaf.  A leaf takes a ring slot at
     // its first push: the < 64 entries left after a drain reference < 64 slots, all among the last
@@ -444,12 +457,14 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan)
     const auto drain = [&]() {
         __builtin_amdgcn_wave_barrier();
+        const unsigned long long d0 = (BRE_PHASE_TIMING && t1 - h1 >= 64) ? phase_clock() : 0ull;
         while (t1 - h1 >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
             if (BRE_ABLATE != 2) tile_exact(sh, h1, 64, srec, sd, seg0, recs, pw, R, count_c);
             h1 += 64;
             __builtin_amdgcn_wave_barrier();
         }
+        if (BRE_PHASE_TIMING && d0 != 0ull) ph_exact += phase_clock() - d0;
         if (h1 >= 1024) {
             h1 -= 1024;
             t1 -= 1024;
@@ -466,6 +481,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pf.beams += nb;
         }
         if (BRE_ABLATE == 4) return;
+        const unsigned long long l0 = phase_clock();
         cur_first = first;
         cur_slot = -1;
         ScanBeam T;
@@ -508,6 +524,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             }
             return;
         }
+        const unsigned long long l1 = phase_clock();
+        if (BRE_PHASE_TIMING) ph_stage += l1 - l0;
+        const unsigned long long ex0 = ph_exact;
         // two kept beams per step: independent broadcasts and prefilters (ILP), then the survivors
         // are queued beam by beam in order (without the prefilter every beam is kept, km = all, and
         // every lane on the leaf's box queues it)
@@ -526,6 +545,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             if (two) push(j2, n2);
             drain();
         }
+        if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
     };
 
     if (__ballot(valid) != 0ull) {
@@ -633,6 +653,12 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pcnt[2 * ((int64_t)sub * nseg + s)] = COUNT ? cand : -1;
             pcnt[2 * ((int64_t)sub * nseg + s) + 1] = sh.cnt[lane];
         }
+    }
+    if (BRE_PHASE_TIMING && !COUNT && lane == 0) {
+        atomicAdd(&ctr->candidates, ph_stage);
+        atomicAdd(&ctr->contributions, ph_scan);
+        atomicAdd(&ctr->node_visits, ph_exact);
+        atomicAdd(&ctr->leaf_visits, phase_clock() - ph_t0);
     }
     if (COUNT) {
         unsigned long long rj = pf.rejects;
