@@ -12,6 +12,6 @@ tail -n 2 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo smoke failed; cat "$OUT/smoke.log"; exit 1; }
 timeout -k 10 600 bash profiles/run_profiles.sh "$OUT/prof" --steps 16 --warmup 2 || { echo profiles failed; exit 1; }
 cat "$OUT/prof/summary.log"
-timeout -k 10 400 python -u bench.py --json-out "$OUT/bench.json" --profile-summary "$OUT/prof/profile_summary.json" \
+timeout -k 10 400 python -u bench.py --json-out "$OUT/bench.json" \
     > "$OUT/bench.log" 2>&1 || { echo bench failed; tail -n 30 "$OUT/bench.log"; exit 1; }
 cat "$OUT/bench.json"
