@@ -84,7 +84,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial, pcnt, segrec;
+    DevMem counters_buf, roots, partial, pcnt, segrec, scanrec;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // camera pass
@@ -421,6 +421,10 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         a.partial = c->partial.as<float>();
         HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)nseg));
         a.segrec = c->segrec.as<SegRec>();
+        if (c->scan_mode == 2) {
+            HIPCHK(c, c->scanrec.ensure(2 * sizeof(float4) * (size_t)c->nvalid));
+            a.scanrec = c->scanrec.as<float4>();
+        }
         if (c->counters || seg_counts) {
             HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
             a.pcnt = c->pcnt.as<int32_t>();
@@ -502,7 +506,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec, &c->scanrec,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -579,8 +583,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
-    case 106:  // internal: tile kernel scan source, 0 LDS / 1 registers (sweeps)
-        if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "scan mode must be 0 or 1");
+    case 106:  // internal: tile kernel scan source, 0 LDS / 1 registers / 2 scalar-loaded records (sweeps)
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "scan mode must be 0, 1 or 2");
         c->scan_mode = (int)value;
         return BRE_OK;
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);

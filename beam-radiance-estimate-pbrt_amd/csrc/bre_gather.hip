@@ -45,6 +45,17 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
+// BRE_SCAN_PIN 1: scan mode 2's record loads are pinned above the step's tests (sched_barrier)
+#ifndef BRE_SCAN_PIN
+#define BRE_SCAN_PIN 0
+#endif
+// BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
+#ifndef BRE_BOX_REJECT
+#define BRE_BOX_REJECT 1
+#endif
+#ifndef BRE_SCAN_ASM
+#define BRE_SCAN_ASM 0
+#endif
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
 #endif
@@ -144,6 +155,11 @@ struct Bundle {
     f3 co, cu;
     float delta;  // FLT_MAX disables the test
     float omax;   // max over valid lanes of Lane::omax (bounds every segment-side coordinate)
+    // packet capsule of the lanes' RAYS [o, o + tmax d] (what the reference's box test sees): every
+    // ray point is co + s cu + w with s in [s0, s1] and |w| <= gbox (rounding margins included);
+    // gbox = FLT_MAX disables the box reject
+    float s0, s1, gbox;
+    f3 icu;       // 1 / cu with infinities replaced by +-FLT_MAX
 };
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -178,11 +194,54 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
     const float cm = fmaxf(fmaxf(fabsf(K.co.x), fabsf(K.co.y)), fabsf(K.co.z));
     const float d = wave_max(dl);
     K.delta = (ok && isfinite(d)) ? d * 1.0001f + 1e-5f * (K.omax + cm) + 1e-6f : FLT_MAX;
+    // the rays' capsule around C for the box reject (bundle_box_miss)
+    {
+        const f3 q = add3(L.o, scale3(L.d, L.tmax));  // far end of the reference's ray extent
+        const float qm = fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fabsf(q.z));
+        const bool fin = !valid || (isfinite(qm) && isfinite(L.omax));
+        const float so = dot3(sub3(L.o, K.co), K.cu), sq = dot3(sub3(q, K.co), K.cu);
+        const float db = valid ? fmaxf(perp(L.o), perp(q)) : 0.f;
+        const float dmax = wave_max(db);
+        const float smax = wave_max(valid ? fmaxf(so, sq) : -FLT_MAX);
+        const float smin = -wave_max(valid ? -fminf(so, sq) : -FLT_MAX);
+        const float mb = fmaxf(K.omax, wave_max(valid ? qm : 0.f)) + cm;
+        const bool all_fin = __ballot(!fin) == 0ull;
+        const float mg = 1e-5f * mb + 1e-6f;
+        K.gbox = (ok && all_fin && isfinite(dmax) && isfinite(mb)) ? dmax * 1.0001f + mg : FLT_MAX;
+        K.s0 = smin - mg;
+        K.s1 = smax + mg;
+        K.icu = mk(sanitize_inv(1.0f / K.cu.x), sanitize_inv(1.0f / K.cu.y), sanitize_inv(1.0f / K.cu.z));
+    }
     K.co = mk(uniform_f(K.co.x), uniform_f(K.co.y), uniform_f(K.co.z));
     K.cu = mk(uniform_f(K.cu.x), uniform_f(K.cu.y), uniform_f(K.cu.z));
     K.delta = uniform_f(K.delta);
     K.omax = uniform_f(K.omax);
+    K.gbox = uniform_f(K.gbox);
+    K.s0 = uniform_f(K.s0);
+    K.s1 = uniform_f(K.s1);
+    K.icu = mk(uniform_f(K.icu.x), uniform_f(K.icu.y), uniform_f(K.icu.z));
     return K;
+}
+
+// Packet-level box reject.  A pair is a candidate only if the lane's ray hits the beam's (group) box
+// (the reference's slab test, photonbeambvh.cpp:685-723); every lane's ray lies in the capsule
+// {co + s cu + w : s in [s0, s1], |w| <= gbox}, which meets the box only if the piece C[s0, s1]
+// crosses the box grown by gbox.  If it does not, no lane can hit the box (gbox and the s-range carry
+// 1e-5 of the coordinate bound: far above the reference test's own rounding and its gamma(3)
+// far-plane pad), so the beam is no lane's candidate and is skipped for the whole packet.
+// A box with a NaN coordinate is never rejected here.
+__device__ __forceinline__ bool bundle_box_miss(const Bundle &K, const Box6 &b) {
+    if (!(K.gbox < 1e30f)) return false;
+    // A plane within ~gbox of the capsule has |coordinate| <= ~2 x the packet's coordinate bound, so
+    // the packet-side margin already covers its rounding; farther planes cannot flip the decision.
+    const float bsum = (b.lx + b.ly) + (b.lz + b.hx) + (b.hy + b.hz);
+    const float g = K.gbox;
+    const float ax = (b.lx - g - K.co.x) * K.icu.x, cx = (b.hx + g - K.co.x) * K.icu.x;
+    const float ay = (b.ly - g - K.co.y) * K.icu.y, cy = (b.hy + g - K.co.y) * K.icu.y;
+    const float az = (b.lz - g - K.co.z) * K.icu.z, cz = (b.hz + g - K.co.z) * K.icu.z;
+    const float tn = fmaxf(fmaxf(fminf(ax, cx), fminf(ay, cy)), fmaxf(fminf(az, cz), K.s0));
+    const float tf = fminf(fminf(fmaxf(ax, cx), fmaxf(ay, cy)), fminf(fmaxf(az, cz), K.s1));
+    return (bsum == bsum) & (tn > tf);
 }
 
 // far_from_lines_fast's bound (bre_lane.h) for the bundle's line against a beam line, with
@@ -299,6 +358,41 @@ __device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j
     return B;
 }
 
+// Beam j's scan values from the per-gather scan records (k_scan_prep, two float4 per beam: (bu, Ab'),
+// (m0, 0)).  `row` and j are wave-uniform, so these are scalar loads into SGPRs: the scan's beam
+// operands never pass through LDS or VALU.
+__device__ __forceinline__ ScanBeam scan_beam_rec(const float4 *__restrict__ row, int j) {
+    const float4 a = row[2 * j], b = row[2 * j + 1];
+    ScanBeam B;
+    B.bu = mk(a.x, a.y, a.z);
+    B.ab = a.w + b.w;  // b.w = 0: one 32-B load per beam
+    B.m0 = mk(b.x, b.y, b.z);
+    return B;
+}
+
+#if BRE_SCAN_ASM
+// Scan mode 2 with explicit scalar-load pipelining (profiling variant): the next step's records are
+// requested by an s_load the compiler does not track, and consumed only after an explicit
+// lgkmcnt(0) wait that also "modifies" them, so nothing reads them early.
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u32x8 sload_rec(const float4 *row, int j) {
+    u32x8 r;
+    const float4 *p = row + 2 * j;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(r) : "s"(p) : "memory");
+    return r;
+}
+__device__ __forceinline__ void swait2(u32x8 &a, u32x8 &b) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b) : : "memory");
+}
+__device__ __forceinline__ ScanBeam unpack_rec(const u32x8 &r) {
+    ScanBeam B;
+    B.bu = mk(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]));
+    B.ab = __uint_as_float(r[3]);
+    B.m0 = mk(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]));
+    return B;
+}
+#endif
+
 // Branch-free (no early exit for near-parallel pairs): the beam's values can be read in one go and
 // two beams' tests interleave.  fma(-c, c, 1.00001) > 0 for unit vectors, so nl is never NaN.
 __device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, const ScanBeam &B) {
@@ -387,13 +481,13 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
 // C), plus traversal statistics; the queue of pairs and hence every sum are the same as without.
 // pcnt (runtime, wave-uniform): count the contributions per segment in the production
 // instantiation, with the production control flow (per-subtree counts in pcnt[.][1]).
-template <bool COUNT, int MINW, bool SCAN_LDS>
+template <bool COUNT, int MINW, int SCAN>
 __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter) {
+    DevCounters *ctr, int stack_cap, int prefilter, const float4 *__restrict__ scanrec) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  Blocks b and b+8 share an XCD under the observed round-robin
     // dispatch, so for S >= 8 XCD (b & 7) is given the S/8 consecutive work roots below one depth-3
@@ -490,14 +584,14 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         bool keep = false;
         if (lane < nb) {
             const BeamV r = load_beam(recs, first + lane);
-            T = make_scan_beam(r, R);
+            if (SCAN != 2) T = make_scan_beam(r, R);
             // packet-level bundle reject (see make_bundle): a beam far from every segment of the
             // packet is skipped by all lanes
-            keep = !prefilter || !bundle_far(K, r.b0, r.bu, R + r.radius);
+            keep = !prefilter || !(bundle_far(K, r.b0, r.bu, R + r.radius) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
         }
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
-        if (SCAN_LDS) {
+        if (SCAN == 0) {
             __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
             if (lane < nb) {
                 sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, T.ab);
@@ -505,7 +599,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             }
             __builtin_amdgcn_wave_barrier();
         }
-        const auto beam_of = [&](int j) { return SCAN_LDS ? scan_beam_lds(sh.tile, j) : scan_beam_of(T, j); };
+        const float4 *__restrict__ srow = scanrec + 2 * first;  // SCAN 2: this tile's scan records
+        const auto beam_of = [&](int j) {
+            return SCAN == 2 ? scan_beam_rec(srow, j) : SCAN == 0 ? scan_beam_lds(sh.tile, j) : scan_beam_of(T, j);
+        };
         if (COUNT) {
             pf.useful += __popcll(km);
             // every beam of the tile: the reference box test (candidates) and the pairs the
@@ -531,14 +628,88 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // are queued beam by beam in order (without the prefilter every beam is kept, km = all, and
         // every lane on the leaf's box queues it)
         unsigned long long todo = km;
-        while (todo != 0ull) {
+#if BRE_SCAN_ASM
+        if (SCAN == 2 && todo != 0ull) {
+            int j1 = __ffsll((long long)todo) - 1;
+            todo &= todo - 1ull;
+            bool two = todo != 0ull;
+            int j2 = two ? __ffsll((long long)todo) - 1 : j1;
+            if (two) todo &= todo - 1ull;
+            u32x8 R1 = sload_rec(srow, j1), R2 = sload_rec(srow, j2);
+            swait2(R1, R2);
+            while (true) {
+                const bool more = todo != 0ull;
+                const int k1 = more ? __ffsll((long long)todo) - 1 : j1;
+                if (more) todo &= todo - 1ull;
+                const bool two_n = todo != 0ull;
+                const int k2 = two_n ? __ffsll((long long)todo) - 1 : k1;
+                if (two_n) todo &= todo - 1ull;
+                u32x8 N1 = sload_rec(srow, k1), N2 = sload_rec(srow, k2);
+                const ScanBeam B1 = unpack_rec(R1), B2 = unpack_rec(R2);
+                const bool pf = prefilter != 0;
+                const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
+                const bool n1 = lane_on && !f1;
+                const bool n2 = two && lane_on && !f2;
+                push(j1, n1);
+                if (two) push(j2, n2);
+                drain();
+                swait2(N1, N2);
+                if (!more) break;
+                j1 = k1;
+                j2 = k2;
+                two = two_n;
+                R1 = N1;
+                R2 = N2;
+            }
+        }
+#else
+        if (SCAN == 2 && todo != 0ull) {
+            // the same steps, software-pipelined: the next step's two records are loaded (scalar loads,
+            // wave-uniform) before this step's prefilters run, so their latency hides behind them
+            int j1 = __ffsll((long long)todo) - 1;
+            todo &= todo - 1ull;
+            bool two = todo != 0ull;
+            int j2 = two ? __ffsll((long long)todo) - 1 : j1;
+            if (two) todo &= todo - 1ull;
+            ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);
+            while (true) {
+                const bool more = todo != 0ull;
+                const int k1 = more ? __ffsll((long long)todo) - 1 : j1;
+                if (more) todo &= todo - 1ull;
+                const bool two_n = todo != 0ull;
+                const int k2 = two_n ? __ffsll((long long)todo) - 1 : k1;
+                if (two_n) todo &= todo - 1ull;
+                const ScanBeam N1 = beam_of(k1), N2 = beam_of(k2);  // issued ahead of this step's tests
+#if BRE_SCAN_PIN
+                __builtin_amdgcn_sched_barrier(0);  // keep the loads above the tests
+#endif
+                // branch-free (the prefilter flag is applied after the tests): the loads, both tests
+                // and the ballots stay in one block, so nothing sinks the loads below the tests
+                const bool pf = prefilter != 0;
+                const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
+                const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
+                const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
+                push(j1, n1);
+                if (two) push(j2, n2);
+                drain();
+                if (!more) break;
+                j1 = k1;
+                j2 = k2;
+                two = two_n;
+                B1 = N1;
+                B2 = N2;
+            }
+        }
+#endif
+        while (SCAN != 2 && todo != 0ull) {
             const int j1 = __ffsll((long long)todo) - 1;
             todo &= todo - 1ull;
             const bool two = todo != 0ull;
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
             const ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);  // both beams' reads issued together
-            const bool f1 = prefilter && scan_far(SL, L.au, B1), f2 = prefilter && scan_far(SL, L.au, B2);
+            const bool pf = prefilter != 0;  // branch-free: both tests in one block (packed by the compiler)
+            const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
             const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
             const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
             push(j1, n1);
@@ -673,6 +844,17 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             atomicAdd(&ctr->ccp_wave_evals, pf.ccp_waves);
         }
     }
+}
+
+// Per-gather scan records of the beams (scan mode 2): (bu, Ab'), (m0, 0) with maxd = R + r folded
+// into Ab' -- the values make_scan_beam gives the other scan modes, bit for bit.
+__global__ __launch_bounds__(256) void k_scan_prep(int64_t n, const BeamRec *__restrict__ recs, float R,
+                                                   float4 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const ScanBeam B = make_scan_beam(load_beam(recs, i), R);
+    out[2 * i] = make_float4(B.bu.x, B.bu.y, B.bu.z, B.ab);
+    out[2 * i + 1] = make_float4(B.m0.x, B.m0.y, B.m0.z, 0.f);
 }
 
 // One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec): the values
@@ -897,15 +1079,22 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
-#define BRE_LAUNCH_TILE(C, W)                                                                                    \
-    if (a.scan_mode == 1)                                                                                        \
-        hipLaunchKernelGGL((k_gather_tile<C, W, false>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d,   \
-                           a.tmax, a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size,   \
-                           a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter);                                 \
-    else                                                                                                         \
-    hipLaunchKernelGGL((k_gather_tile<C, W, true>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,       \
+    if (a.scan_mode == 2) {
+        if (!a.scanrec) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_scan_prep, dim3((unsigned int)((a.nvalid + 255) / 256)), dim3(256), 0, s, a.nvalid,
+                           a.recs, a.R, a.scanrec);
+    }
+#define BRE_LAUNCH_TILE_M(C, W, M)                                                                               \
+    hipLaunchKernelGGL((k_gather_tile<C, W, M>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,   \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter)
+                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.scanrec)
+#define BRE_LAUNCH_TILE(C, W)                                                                                    \
+    if (a.scan_mode == 2)                                                                                        \
+        BRE_LAUNCH_TILE_M(C, W, 2);                                                                              \
+    else if (a.scan_mode == 1)                                                                                   \
+        BRE_LAUNCH_TILE_M(C, W, 1);                                                                              \
+    else                                                                                                         \
+        BRE_LAUNCH_TILE_M(C, W, 0)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {
@@ -918,6 +1107,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         BRE_LAUNCH_TILE(false, 8);
     }
 #undef BRE_LAUNCH_TILE
+#undef BRE_LAUNCH_TILE_M
     hipError_t e4 = hipGetLastError();
     if (e4 != hipSuccess) return e4;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial, pcnt,

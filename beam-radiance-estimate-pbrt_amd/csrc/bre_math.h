@@ -32,12 +32,14 @@ __host__ __device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + 
 __host__ __device__ __forceinline__ float lensq3(f3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 __host__ __device__ __forceinline__ float len3(f3 a) { return sqrtf(lensq3(a)); }
 
-// Cross(v1, v2) in double, geometry.h:957-963
+// Cross(v1, v2) in double, geometry.h:957-963.  A product of two floats is exact in double (24 + 24
+// significant bits <= 53), so (a*b) - (c*d) with both products rounded is fma(a, b, -(c*d)): the same
+// single rounding of the exact difference, one double instruction less per component.
 __host__ __device__ __forceinline__ f3 cross3d(f3 v1, f3 v2) {
     const double v1x = v1.x, v1y = v1.y, v1z = v1.z;
     const double v2x = v2.x, v2y = v2.y, v2z = v2.z;
-    return mk((float)((v1y * v2z) - (v1z * v2y)), (float)((v1z * v2x) - (v1x * v2z)),
-              (float)((v1x * v2y) - (v1y * v2x)));
+    return mk((float)__builtin_fma(v1y, v2z, -(v1z * v2y)), (float)__builtin_fma(v1z, v2x, -(v1x * v2z)),
+              (float)__builtin_fma(v1x, v2y, -(v1y * v2x)));
 }
 
 // Determinant, photonbeam.cpp:79-85
