@@ -57,10 +57,10 @@ struct bre_ctx {
     int kernel = 0;
     int leaf_size = 1;
     int sqrt_mode = 0;
-    int split = 8;
+    int split = 64;          // work roots per packet (r2: 64 with the rotated block map, C2 +42% over 8)
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
-    int scan_mode = 0;       // internal: tile kernel scan source (GatherArgs::scan_mode)
+    int block_map = 1;       // internal: tile kernel block mapping (GatherArgs::block_map): 1 rotated
     int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best at C2 (r2)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
@@ -84,7 +84,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial, pcnt, segrec, scanrec;
+    DevMem counters_buf, roots, partial, pcnt, segrec;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // camera pass
@@ -396,8 +396,8 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.split = c->split;
     a.prefilter = c->prefilter;
     a.occupancy = c->occupancy;
+    a.block_map = c->block_map;
     a.stack_cap = c->stack_cap;
-    a.scan_mode = c->scan_mode;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
         // empty PhotonBeamBVH: Intersect returns nothing (photonbeambvh.cpp:687)
@@ -421,10 +421,6 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         a.partial = c->partial.as<float>();
         HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)nseg));
         a.segrec = c->segrec.as<SegRec>();
-        if (c->scan_mode == 2) {
-            HIPCHK(c, c->scanrec.ensure(2 * sizeof(float4) * (size_t)c->nvalid));
-            a.scanrec = c->scanrec.as<float4>();
-        }
         if (c->counters || seg_counts) {
             HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
             a.pcnt = c->pcnt.as<int32_t>();
@@ -506,7 +502,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec, &c->scanrec,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -583,9 +579,9 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
-    case 106:  // internal: tile kernel scan source, 0 LDS / 1 registers / 2 scalar-loaded records (sweeps)
-        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "scan mode must be 0, 1 or 2");
-        c->scan_mode = (int)value;
+    case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated (sweeps)
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0, 1 or 2");
+        c->block_map = (int)value;
         return BRE_OK;
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }

@@ -139,9 +139,7 @@ struct GatherArgs {
     bool prefilter;
     int occupancy;         // tile kernel register budget: min waves per SIMD (1, 6, 7 or 8)
     int stack_cap;         // traversal stack entries to use (0 = all); tests force an overflow
-    int scan_mode;         // tile kernel scan: 0 tile staged in LDS, 1 tile in registers + v_readlane,
-                           // 2 per-gather scan records read by scalar loads
-    float4 *scanrec;       // scan mode 2: [nvalid][2] (k_scan_prep)
+    int block_map;         // tile kernel block -> (packet, subtree) mapping (k_gather_tile)
 };
 
 // capsule-chunk index (bre_chunk.hip)

@@ -45,16 +45,9 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
-// BRE_SCAN_PIN 1: scan mode 2's record loads are pinned above the step's tests (sched_barrier)
-#ifndef BRE_SCAN_PIN
-#define BRE_SCAN_PIN 0
-#endif
 // BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
 #ifndef BRE_BOX_REJECT
 #define BRE_BOX_REJECT 1
-#endif
-#ifndef BRE_SCAN_ASM
-#define BRE_SCAN_ASM 0
 #endif
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
@@ -332,19 +325,6 @@ __device__ __forceinline__ ScanBeam make_scan_beam(const BeamV &r, float R) {
     return B;
 }
 
-__device__ __forceinline__ float rdl(float v, int j) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
-
-// Beam j's scan values, broadcast from lane j's registers by v_readlane (wave-uniform: SGPRs).
-__device__ __forceinline__ ScanBeam scan_beam_of(const ScanBeam &T, int j) {
-    ScanBeam B;
-    B.bu = mk(rdl(T.bu.x, j), rdl(T.bu.y, j), rdl(T.bu.z, j));
-    B.m0 = mk(rdl(T.m0.x, j), rdl(T.m0.y, j), rdl(T.m0.z, j));
-    B.ab = rdl(T.ab, j);
-    return B;
-}
-
 // Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128).  The second
 // record's w is a stored 0 added to Ab': without a use the compiler narrows that read to
 // ds_read_b96, which takes 8 LDS cycles per wave instead of ds_read_b128's 4 (MI355X_MICROARCH.md
@@ -358,85 +338,61 @@ __device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j
     return B;
 }
 
-// Beam j's scan values from the per-gather scan records (k_scan_prep, two float4 per beam: (bu, Ab'),
-// (m0, 0)).  `row` and j are wave-uniform, so these are scalar loads into SGPRs: the scan's beam
-// operands never pass through LDS or VALU.
-__device__ __forceinline__ ScanBeam scan_beam_rec(const float4 *__restrict__ row, int j) {
-    const float4 a = row[2 * j], b = row[2 * j + 1];
-    ScanBeam B;
-    B.bu = mk(a.x, a.y, a.z);
-    B.ab = a.w + b.w;  // b.w = 0: one 32-B load per beam
-    B.m0 = mk(b.x, b.y, b.z);
-    return B;
-}
-
-#if BRE_SCAN_ASM
-// Scan mode 2 with explicit scalar-load pipelining (profiling variant): the next step's records are
-// requested by an s_load the compiler does not track, and consumed only after an explicit
-// lgkmcnt(0) wait that also "modifies" them, so nothing reads them early.
-typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ u32x8 sload_rec(const float4 *row, int j) {
-    u32x8 r;
-    const float4 *p = row + 2 * j;
-    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(r) : "s"(p) : "memory");
-    return r;
-}
-__device__ __forceinline__ void swait2(u32x8 &a, u32x8 &b) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b) : : "memory");
-}
-__device__ __forceinline__ ScanBeam unpack_rec(const u32x8 &r) {
-    ScanBeam B;
-    B.bu = mk(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]));
-    B.ab = __uint_as_float(r[3]);
-    B.m0 = mk(__uint_as_float(r[4]), __uint_as_float(r[5]), __uint_as_float(r[6]));
-    return B;
-}
-#endif
-
-// Branch-free (no early exit for near-parallel pairs): the beam's values can be read in one go and
-// two beams' tests interleave.  fma(-c, c, 1.00001) > 0 for unit vectors, so nl is never NaN.
-__device__ __forceinline__ bool scan_far(const ScanLane &S, f3 au, const ScanBeam &B) {
+// The per-(lane, beam) prefilter as ONE comparison, so that its ballot is the compare's own lane
+// mask (no mask materialisation, no exec juggling in the queue push).  The pair is rejected iff
+//   nn_lo >= 1e-2  and  tn > (Ab' + Al') * nl          (the separable bound above)
+// and `need` is the complement.  key = tn, or -1 when nn_lo < 1e-2 (or NaN): -1 > thr never holds
+// (thr > 0), so such pairs are kept, as before.  al_eff folds the lane's leaf visit and the
+// prefilter switch into the threshold: -inf for a lane off the leaf's box (thr = -inf: never
+// queued), +inf with the prefilter off (thr = +inf: always queued), Al' otherwise.
+// fma(-c, c, 1.00001) > 0 for unit vectors, so nl is never NaN.
+__device__ __forceinline__ bool scan_need(const ScanLane &S, float al_eff, f3 au, const ScanBeam &B) {
     const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
     const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
     const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
     const float tn =
         fabsf(__builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x))));
     const float nl = __builtin_amdgcn_sqrtf(__builtin_fmaf(-c, c, 1.00001f)) * 1.000001f + 1e-6f;
-    return (nn_lo >= 1e-2f) & (tn > (B.ab + S.al) * nl);
+    const float key = (nn_lo >= 1e-2f) ? tn : -1.0f;
+    return !(key > (B.ab + al_eff) * nl);
 }
 
 constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
-constexpr int kQueueCap = 256;   // >= 63 left over + 128 appended by one scan step (two beams)
-constexpr int kRing = 64;        // leaf-base ring: queue entries reference < 64 distinct leaves (see push)
+constexpr int kQueueCap = 192;   // >= 63 left over + 128 appended by one scan step (two beams)
+
+// One queued (beam, lane) pair: the beam's index in BVH order and the segment's lane.
+struct QEntry {
+    int32_t beam;
+    int32_t lane;
+};
 
 struct TileShared {
-    float4 tile[64][2];        // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
-    float acc[3][64];          // per-segment RGB accumulators
-    int32_t cnt[64];           // per-segment contribution counts (counters / contribution counting)
-    uint32_t q[kQueueCap];     // prefilter-survivor ring: ring slot << 12 | beam-in-tile << 6 | segment lane
-    int32_t leaf[kRing];       // first beam of the leaf tile each ring slot stands for
+    float4 tile[64][2];          // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
+    float acc[3][64];            // per-segment RGB accumulators
+    int32_t cnt[64];             // per-segment contribution counts (counters / contribution counting)
+    QEntry q[kQueueCap + 64];    // prefilter survivors [0, t1), then one discard slot per lane
     int32_t stk[kStackDepth];
 };
 
-// The exact stage for n queued prefilter survivors (one per lane; all lanes call): the reference's
-// box test on the beam's (group) box, then ComputeClosestPoints + kernel.  The pair's segment comes
-// from its SegRec, the beam line from L2.
+// The exact stage for n queued prefilter survivors q[first, first + n) (one per lane; all lanes
+// call): the reference's box test on the beam's (group) box, then ComputeClosestPoints + kernel.
+// The pair's segment comes from its SegRec, the beam line from L2.
 __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
                                            const float *__restrict__ sd, int64_t seg0,
                                            const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
                                            bool count) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
-    const uint32_t e = sh.q[(first + (on ? lane : 0)) & (kQueueCap - 1)];  // FIFO ring
-    const int sl = (int)(e & 63u);
-    const int64_t b = (int64_t)sh.leaf[e >> 12] + ((e >> 6) & 63u);
+    const QEntry e = sh.q[first + (on ? lane : 0)];  // off lanes (a partial batch) read a valid entry
+    const int sl = e.lane;
+    const int64_t b = e.beam;
     // every load of the pair is issued at once (one memory round trip per batch; most queued pairs
     // pass the box test, so the second half is rarely wasted)
     const float4 *sr = reinterpret_cast<const float4 *>(srec + seg0 + sl);
     const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
     const float4 s0 = sr[0], s3 = sr[3], bx = rb[0], by = rb[1];
     const float4 s1 = sr[1], s2 = sr[2], bz = rb[2], bw = rb[3];
-    const float4 pv = pw[b];  // off lanes (a partial batch) read entry `first`: a valid beam
+    const float4 pv = pw[b];
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
     const float tmax = s0.w;
@@ -481,27 +437,32 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
 // C), plus traversal statistics; the queue of pairs and hence every sum are the same as without.
 // pcnt (runtime, wave-uniform): count the contributions per segment in the production
 // instantiation, with the production control flow (per-subtree counts in pcnt[.][1]).
-template <bool COUNT, int MINW, int SCAN>
+template <bool COUNT, int MINW>
 __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter, const float4 *__restrict__ scanrec) {
+    DevCounters *ctr, int stack_cap, int prefilter, int map) {
     __shared__ TileShared shm[kTileBlock / 64];
-    // Block -> (subtree, packet group).  Blocks b and b+8 share an XCD under the observed round-robin
-    // dispatch, so for S >= 8 XCD (b & 7) is given the S/8 consecutive work roots below one depth-3
-    // node: each XCD's L2 serves one eighth of the tree (speed only, never correctness).
+    // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
+    // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
+    // subtree (balanced however unequal the subtrees are).  map 0: blocks b and b+8 share an XCD,
+    // so for S >= 8 XCD (b & 7) is given the S/8 consecutive work roots below one depth-3 node (its
+    // L2 serves one eighth of the tree).  Speed only, never correctness.
     int sub;
     int64_t grp;
-    if (S >= 8) {
+    if (map == 1) {
+        grp = blockIdx.x / (unsigned)S;
+        sub = (int)((blockIdx.x % (unsigned)S + grp) % (unsigned)S);
+    } else if (map == 2 || S < 8) {
+        sub = (int)(blockIdx.x % (unsigned)S);
+        grp = blockIdx.x / (unsigned)S;
+    } else {
         const unsigned per = (unsigned)S >> 3;
         const unsigned q = blockIdx.x >> 3;
         sub = (int)((blockIdx.x & 7u) * per + q % per);
         grp = q / per;
-    } else {
-        sub = (int)(blockIdx.x % (unsigned)S);
-        grp = blockIdx.x / (unsigned)S;
     }
     if (sub >= roots[S]) return;  // fewer work roots than S (small trees): whole block exits
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -513,6 +474,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const bool valid = load_lane(s, nseg, so, sp_, sd, stmax, L);
     Bundle K;
     K.delta = FLT_MAX;
+    K.gbox = FLT_MAX;
     if (prefilter && __ballot(valid) != 0ull) K = make_bundle(L, valid);
     const ScanLane SL = make_scan_lane(L);
     sh.acc[0][lane] = 0.f;
@@ -523,50 +485,48 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int cand = 0;
     unsigned long long visits = 0;
     Prof pf;
-    int h1 = 0, t1 = 0;        // wave-uniform FIFO ring head / tail
-    int ring_next = 0;         // next leaf-base ring slot
-    int cur_slot = -1;         // ring slot of the current leaf (-1: none yet)
+    int t1 = 0;                // wave-uniform queue length: survivors in q[0, t1)
     int64_t cur_first = 0;     // first beam of the current leaf
     unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
     const unsigned long long ph_t0 = phase_clock();
 
-    // queue the (beam, lane) survivors of beam j of the current leaf.  A leaf takes a ring slot at
-    // its first push: the < 64 entries left after a drain reference < 64 slots, all among the last
-    // 63 assigned, so a kRing = 64 ring never reuses a slot a live entry holds (a scan step pushes
-    // two beams of one leaf, then drains).
+    // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
+    // stores (branch-free), a lane that queues nothing into its own discard slot
     const auto push = [&](int j, bool need) {
         const unsigned long long m = __ballot(need);
         if (m == 0ull) return;
-        if (cur_slot < 0) {
-            cur_slot = ring_next;
-            ring_next = (ring_next + 1) & (kRing - 1);
-            if (lane == 0) sh.leaf[cur_slot] = (int32_t)cur_first;
-        }
-        if (need) {
-            const int pos = (t1 + lanes_below(m)) & (kQueueCap - 1);
-            sh.q[pos] = ((uint32_t)cur_slot << 12) | ((uint32_t)j << 6) | (uint32_t)lane;
-        }
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
+        sh.q[need ? rank : kQueueCap + lane] = QEntry{(int32_t)(cur_first + j), lane};
         t1 += __popcll(m);
     };
-    // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan)
+    // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan),
+    // then move the < 64 left over to the front of the queue
     const auto drain = [&]() {
+        if (t1 < 64) return;
         __builtin_amdgcn_wave_barrier();
-        const unsigned long long d0 = (BRE_PHASE_TIMING && t1 - h1 >= 64) ? phase_clock() : 0ull;
-        while (t1 - h1 >= 64) {
+        const unsigned long long d0 = BRE_PHASE_TIMING ? phase_clock() : 0ull;
+        int h = 0;
+        while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, h1, 64, srec, sd, seg0, recs, pw, R, count_c);
-            h1 += 64;
+            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, R, count_c);
+            h += 64;
             __builtin_amdgcn_wave_barrier();
         }
-        if (BRE_PHASE_TIMING && d0 != 0ull) ph_exact += phase_clock() - d0;
-        if (h1 >= 1024) {
-            h1 -= 1024;
-            t1 -= 1024;
+        const int rest = t1 - h;  // h >= 64 > rest: source and destination do not overlap
+        if (rest > 0) {
+            QEntry e{0, 0};
+            if (lane < rest) e = sh.q[h + lane];
+            __builtin_amdgcn_wave_barrier();
+            if (lane < rest) sh.q[lane] = e;
+            __builtin_amdgcn_wave_barrier();
         }
+        t1 = rest;
+        if (BRE_PHASE_TIMING) ph_exact += phase_clock() - d0;
     };
 
-    // scan one leaf tile (<= 64 beams): lane j holds beam j's scan values; bundle reject; per lane the
-    // separable prefilter on the kept beams; survivors queue for the exact stage
+    // scan one leaf tile (<= 64 beams): lane j stages beam j's scan values in LDS; bundle rejects;
+    // per lane the separable prefilter on the kept beams; survivors queue for the exact stage
     const auto leaf = [&](int32_t c, bool lane_on) {
         const int64_t first = (int64_t)(~c) * leaf_size;
         const int nb = (int)min((int64_t)leaf_size, nvalid - first);
@@ -577,46 +537,42 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         if (BRE_ABLATE == 4) return;
         const unsigned long long l0 = phase_clock();
         cur_first = first;
-        cur_slot = -1;
         ScanBeam T;
         T.bu = T.m0 = mk(0.f, 0.f, 0.f);
         T.ab = 0.f;
         bool keep = false;
         if (lane < nb) {
             const BeamV r = load_beam(recs, first + lane);
-            if (SCAN != 2) T = make_scan_beam(r, R);
-            // packet-level bundle reject (see make_bundle): a beam far from every segment of the
-            // packet is skipped by all lanes
-            keep = !prefilter || !(bundle_far(K, r.b0, r.bu, R + r.radius) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
+            T = make_scan_beam(r, R);
+            // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
+            // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
+            keep = !prefilter ||
+                   !(bundle_far(K, r.b0, r.bu, R + r.radius) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
         }
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
-        if (SCAN == 0) {
-            __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
-            if (lane < nb) {
-                sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, T.ab);
-                sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
-            }
-            __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
+        if (lane < nb) {
+            sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, T.ab);
+            sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
         }
-        const float4 *__restrict__ srow = scanrec + 2 * first;  // SCAN 2: this tile's scan records
-        const auto beam_of = [&](int j) {
-            return SCAN == 2 ? scan_beam_rec(srow, j) : SCAN == 0 ? scan_beam_lds(sh.tile, j) : scan_beam_of(T, j);
-        };
+        __builtin_amdgcn_wave_barrier();
+        // the lane's threshold term for this tile (see scan_need)
+        const float al_eff = !lane_on ? -INFINITY : (prefilter ? SL.al : INFINITY);
         if (COUNT) {
             pf.useful += __popcll(km);
             // every beam of the tile: the reference box test (candidates) and the pairs the
             // prefilters drop; the queue gets exactly the production survivors, in order
             for (int j = 0; j < nb; ++j) {
-                bool need = lane_on && ((km >> j) & 1ull);
-                if (prefilter && need) need = !scan_far(SL, L.au, beam_of(j));
+                const bool kept = (km >> j) & 1ull;
+                const bool need = kept && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
                 const Box6 box = load_beam(recs, first + j).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                 if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
                 cand += hit;
                 pf.rejects += hit & !need;
-                push(j, need);
+                if (kept) push(j, need);
                 drain();
             }
             return;
@@ -624,94 +580,18 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const unsigned long long l1 = phase_clock();
         if (BRE_PHASE_TIMING) ph_stage += l1 - l0;
         const unsigned long long ex0 = ph_exact;
-        // two kept beams per step: independent broadcasts and prefilters (ILP), then the survivors
-        // are queued beam by beam in order (without the prefilter every beam is kept, km = all, and
-        // every lane on the leaf's box queues it)
+        // two kept beams per step: independent reads and prefilters (ILP, packed by the compiler), then
+        // the survivors are queued beam by beam in order
         unsigned long long todo = km;
-#if BRE_SCAN_ASM
-        if (SCAN == 2 && todo != 0ull) {
-            int j1 = __ffsll((long long)todo) - 1;
-            todo &= todo - 1ull;
-            bool two = todo != 0ull;
-            int j2 = two ? __ffsll((long long)todo) - 1 : j1;
-            if (two) todo &= todo - 1ull;
-            u32x8 R1 = sload_rec(srow, j1), R2 = sload_rec(srow, j2);
-            swait2(R1, R2);
-            while (true) {
-                const bool more = todo != 0ull;
-                const int k1 = more ? __ffsll((long long)todo) - 1 : j1;
-                if (more) todo &= todo - 1ull;
-                const bool two_n = todo != 0ull;
-                const int k2 = two_n ? __ffsll((long long)todo) - 1 : k1;
-                if (two_n) todo &= todo - 1ull;
-                u32x8 N1 = sload_rec(srow, k1), N2 = sload_rec(srow, k2);
-                const ScanBeam B1 = unpack_rec(R1), B2 = unpack_rec(R2);
-                const bool pf = prefilter != 0;
-                const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
-                const bool n1 = lane_on && !f1;
-                const bool n2 = two && lane_on && !f2;
-                push(j1, n1);
-                if (two) push(j2, n2);
-                drain();
-                swait2(N1, N2);
-                if (!more) break;
-                j1 = k1;
-                j2 = k2;
-                two = two_n;
-                R1 = N1;
-                R2 = N2;
-            }
-        }
-#else
-        if (SCAN == 2 && todo != 0ull) {
-            // the same steps, software-pipelined: the next step's two records are loaded (scalar loads,
-            // wave-uniform) before this step's prefilters run, so their latency hides behind them
-            int j1 = __ffsll((long long)todo) - 1;
-            todo &= todo - 1ull;
-            bool two = todo != 0ull;
-            int j2 = two ? __ffsll((long long)todo) - 1 : j1;
-            if (two) todo &= todo - 1ull;
-            ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);
-            while (true) {
-                const bool more = todo != 0ull;
-                const int k1 = more ? __ffsll((long long)todo) - 1 : j1;
-                if (more) todo &= todo - 1ull;
-                const bool two_n = todo != 0ull;
-                const int k2 = two_n ? __ffsll((long long)todo) - 1 : k1;
-                if (two_n) todo &= todo - 1ull;
-                const ScanBeam N1 = beam_of(k1), N2 = beam_of(k2);  // issued ahead of this step's tests
-#if BRE_SCAN_PIN
-                __builtin_amdgcn_sched_barrier(0);  // keep the loads above the tests
-#endif
-                // branch-free (the prefilter flag is applied after the tests): the loads, both tests
-                // and the ballots stay in one block, so nothing sinks the loads below the tests
-                const bool pf = prefilter != 0;
-                const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
-                const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
-                const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
-                push(j1, n1);
-                if (two) push(j2, n2);
-                drain();
-                if (!more) break;
-                j1 = k1;
-                j2 = k2;
-                two = two_n;
-                B1 = N1;
-                B2 = N2;
-            }
-        }
-#endif
-        while (SCAN != 2 && todo != 0ull) {
+        while (todo != 0ull) {
             const int j1 = __ffsll((long long)todo) - 1;
             todo &= todo - 1ull;
             const bool two = todo != 0ull;
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
-            const ScanBeam B1 = beam_of(j1), B2 = beam_of(j2);  // both beams' reads issued together
-            const bool pf = prefilter != 0;  // branch-free: both tests in one block (packed by the compiler)
-            const bool f1 = pf & scan_far(SL, L.au, B1), f2 = pf & scan_far(SL, L.au, B2);
-            const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : !f1);
-            const bool n2 = two && lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : !f2);
+            const ScanBeam B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
+            const bool n1 = BRE_ABLATE == 3 ? lane_on && ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1);
+            const bool n2 = BRE_ABLATE == 3 ? lane_on && ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2);
             push(j1, n1);
             if (two) push(j2, n2);
             drain();
@@ -808,11 +688,11 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         }
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
-        if (t1 > h1) {
+        if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_exact(sh, h1, t1 - h1, srec, sd, seg0, recs, pw, R, count_c);
+            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, R, count_c);
         }
-        h1 = t1 = 0;
+        t1 = 0;
     }
     __builtin_amdgcn_wave_barrier();
     if (valid) {
@@ -844,17 +724,6 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             atomicAdd(&ctr->ccp_wave_evals, pf.ccp_waves);
         }
     }
-}
-
-// Per-gather scan records of the beams (scan mode 2): (bu, Ab'), (m0, 0) with maxd = R + r folded
-// into Ab' -- the values make_scan_beam gives the other scan modes, bit for bit.
-__global__ __launch_bounds__(256) void k_scan_prep(int64_t n, const BeamRec *__restrict__ recs, float R,
-                                                   float4 *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const ScanBeam B = make_scan_beam(load_beam(recs, i), R);
-    out[2 * i] = make_float4(B.bu.x, B.bu.y, B.bu.z, B.ab);
-    out[2 * i + 1] = make_float4(B.m0.x, B.m0.y, B.m0.z, 0.f);
 }
 
 // One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec): the values
@@ -1079,35 +948,22 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
-    if (a.scan_mode == 2) {
-        if (!a.scanrec) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_scan_prep, dim3((unsigned int)((a.nvalid + 255) / 256)), dim3(256), 0, s, a.nvalid,
-                           a.recs, a.R, a.scanrec);
-    }
-#define BRE_LAUNCH_TILE_M(C, W, M)                                                                               \
-    hipLaunchKernelGGL((k_gather_tile<C, W, M>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,   \
-                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.scanrec)
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
-    if (a.scan_mode == 2)                                                                                        \
-        BRE_LAUNCH_TILE_M(C, W, 2);                                                                              \
-    else if (a.scan_mode == 1)                                                                                   \
-        BRE_LAUNCH_TILE_M(C, W, 1);                                                                              \
-    else                                                                                                         \
-        BRE_LAUNCH_TILE_M(C, W, 0)
+    hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
+                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
+                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {
         BRE_LAUNCH_TILE(false, 1);
     } else if (a.occupancy == 6) {
         BRE_LAUNCH_TILE(false, 6);
-    } else if (a.occupancy == 7) {
-        BRE_LAUNCH_TILE(false, 7);
-    } else {
+    } else if (a.occupancy == 8) {
         BRE_LAUNCH_TILE(false, 8);
+    } else {
+        BRE_LAUNCH_TILE(false, 7);
     }
 #undef BRE_LAUNCH_TILE
-#undef BRE_LAUNCH_TILE_M
     hipError_t e4 = hipGetLastError();
     if (e4 != hipSuccess) return e4;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial, pcnt,

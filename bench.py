@@ -72,7 +72,7 @@ def parse(argv=None):
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=1)
-    ap.add_argument("--split", type=int, default=8, help="BVH subtrees per segment packet")
+    ap.add_argument("--split", type=int, default=64, help="BVH subtrees (work roots) per segment packet")
     ap.add_argument("--prefilter", type=int, default=1)
     ap.add_argument("--chunk-len", type=int, default=400, help="kernel 5: chunk length in units of E/100")
     ap.add_argument("--chunk-leaf", type=int, default=1, help="kernel 5: chunks per LBVH leaf")
@@ -80,7 +80,7 @@ def parse(argv=None):
     ap.add_argument("--occupancy", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
-    ap.add_argument("--scan-mode", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -169,10 +169,10 @@ def main():
         g.set_option(102, args.occupancy)
     if args.tile_leaf:
         g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
+    if args.block_map >= 0:
+        g.set_option(107, args.block_map)
     if args.sort_key >= 0:
         g.set_option(105, args.sort_key)
-    if args.scan_mode >= 0:
-        g.set_option(106, args.scan_mode)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)
