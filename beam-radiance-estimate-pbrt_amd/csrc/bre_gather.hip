@@ -34,10 +34,10 @@ namespace {
 
 constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 
-// Profiling ablations (compile-time, off in the product; profiles/ablate.sh builds them into
-// separate libraries): BRE_ABLATE 1 = exact stage without the LDS float atomics (plain stores:
-// wrong sums), 2 = no exact stage (queue drained unread), 3 = no prefilter scan (every kept beam's
-// prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf tiles not scanned).
+// Profiling ablations (compile-time, off in the product; profiles/variant.sh builds them into
+// separate libraries): BRE_ABLATE 2 = no exact stage (queue drained unread), 3 = no prefilter scan
+// (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
+// tiles not scanned).
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
 #endif
@@ -368,8 +368,7 @@ struct QEntry {
 
 struct TileShared {
     float4 tile[64][2];          // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
-    float acc[3][64];            // per-segment RGB accumulators
-    int32_t cnt[64];             // per-segment contribution counts (counters / contribution counting)
+    float4 acc[64];              // per-segment RGB sums and contribution count (w, exact below 2^24)
     QEntry q[kQueueCap + 64];    // prefilter survivors [0, t1), then one discard slot per lane
     int32_t stk[kStackDepth];
 };
@@ -411,6 +410,8 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     }
     if (__ballot(hit) == 0ull) return;
     // phase 2: closest points + kernel
+    float4 v = make_float4(0.f, 0.f, 0.f, 1.f);
+    bool contrib = false;
     if (hit) {
         const float maxd = R + bw.y;  // MaxDistance = currentBeamRadius + beam->radius
         float dist;
@@ -419,16 +420,35 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
             const float w = sqrtf(1.0f - rr * rr);
-            if (BRE_ABLATE == 1) {
-                sh.acc[0][sl] = pv.x * w;
-                sh.acc[1][sl] = pv.y * w;
-                sh.acc[2][sl] = pv.z * w;
-            } else {
-                atomicAdd(&sh.acc[0][sl], pv.x * w);
-                atomicAdd(&sh.acc[1][sl], pv.y * w);
-                atomicAdd(&sh.acc[2][sl], pv.z * w);
-            }
-            if (count) atomicAdd(&sh.cnt[sl], 1);
+            v.x = pv.x * w;
+            v.y = pv.y * w;
+            v.z = pv.z * w;
+            contrib = true;
+        }
+    }
+    // Accumulate into the segments' LDS sums without atomics.  The batch is the queue in order: runs
+    // of one beam's pairs, each run in increasing segment lane (push), so the segment lanes inside a
+    // run are distinct.  Run by run, the run's contributing lanes read-modify-write their segment's
+    // float4 (one wave's LDS accesses are performed in order): each segment's terms are added in
+    // queue order.  (`count` only decides whether the count is used: it is always kept.)
+    (void)count;
+    const unsigned long long cm = __ballot(contrib);
+    if (cm == 0ull) return;
+    const int prev = __shfl_up(e.beam, 1);
+    unsigned long long starts = __ballot(lane == 0 || e.beam != prev);
+    while (starts != 0ull) {
+        const int s0 = __ffsll((long long)starts) - 1;
+        starts &= starts - 1ull;
+        const unsigned long long upto = starts != 0ull ? (1ull << (__ffsll((long long)starts) - 1)) - 1ull : ~0ull;
+        const unsigned long long run = cm & upto & ~((1ull << s0) - 1ull);
+        if (run == 0ull) continue;
+        if ((run >> lane) & 1ull) {
+            float4 a = sh.acc[sl];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+            sh.acc[sl] = a;
         }
     }
 }
@@ -477,10 +497,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     K.gbox = FLT_MAX;
     if (prefilter && __ballot(valid) != 0ull) K = make_bundle(L, valid);
     const ScanLane SL = make_scan_lane(L);
-    sh.acc[0][lane] = 0.f;
-    sh.acc[1][lane] = 0.f;
-    sh.acc[2][lane] = 0.f;
-    sh.cnt[lane] = 0;
+    sh.acc[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     __builtin_amdgcn_wave_barrier();
     int cand = 0;
     unsigned long long visits = 0;
@@ -603,7 +620,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const int32_t root = roots[sub];
         // the production instantiation re-reads the lane's o, tmax and 1/d from its SegRec at each
         // node visit instead of holding them in VGPRs through the leaf scans (register budget)
-        const float4 *my = reinterpret_cast<const float4 *>(srec + (s < nseg ? s : nseg - 1));
+        const int my = (int)(s < nseg ? s : nseg - 1);  // this lane's SegRec (index: one VGPR)
         // Leaf children found at a node visit are scanned at the top of the next step, c0's before
         // c1's, so the leaf scan (and the exact stage inside it) is inlined once.
         int32_t lc0 = 0, lc1 = 0;
@@ -634,10 +651,11 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             f3 lo = L.o, li = L.invs;
             float lt = L.tmax;
             if (!COUNT) {
-                // an opaque copy of the address per visit: keeps the compiler from hoisting the
-                // two loads out of the loop (and the 7 values back into registers)
-                const float4 *mp = my;
-                asm volatile("" : "+v"(mp));
+                // an opaque copy of the index per visit: keeps the compiler from hoisting the two
+                // loads out of the loop (and the 7 values back into registers)
+                int mi = my;
+                asm volatile("" : "+v"(mi));
+                const float4 *mp = reinterpret_cast<const float4 *>(srec + mi);
                 const float4 a0 = mp[0], a3 = mp[3];
                 lo = mk(a0.x, a0.y, a0.z);
                 lt = a0.w;
@@ -697,12 +715,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     __builtin_amdgcn_wave_barrier();
     if (valid) {
         float *dst = partial + 3 * ((int64_t)sub * nseg + s);
-        dst[0] = sh.acc[0][lane];
-        dst[1] = sh.acc[1][lane];
-        dst[2] = sh.acc[2][lane];
+        const float4 a = sh.acc[lane];
+        dst[0] = a.x;
+        dst[1] = a.y;
+        dst[2] = a.z;
         if (count_c) {
             pcnt[2 * ((int64_t)sub * nseg + s)] = COUNT ? cand : -1;
-            pcnt[2 * ((int64_t)sub * nseg + s) + 1] = sh.cnt[lane];
+            pcnt[2 * ((int64_t)sub * nseg + s) + 1] = (int32_t)a.w;
         }
     }
     if (BRE_PHASE_TIMING && !COUNT && lane == 0) {
