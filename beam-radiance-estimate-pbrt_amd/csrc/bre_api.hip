@@ -61,7 +61,7 @@ struct bre_ctx {
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
     int block_map = 1;       // internal: tile kernel block mapping (GatherArgs::block_map): 1 rotated
-    int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best at C2 (r2)
+    int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 measured best (r2, per-run RMW build)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
@@ -574,8 +574,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->stack_cap = (int)value;
         return BRE_OK;
     case 102:  // internal: tile kernel register budget, min waves per SIMD (sweeps)
-        if (value != 1 && value != 6 && value != 7 && value != 8)
-            return fail(c, BRE_ERR_INVALID_ARG, "occupancy must be 1, 6, 7 or 8");
+        if (value != 1 && (value < 4 || value > 8))
+            return fail(c, BRE_ERR_INVALID_ARG, "occupancy must be 1 or 4..8");
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)

@@ -45,6 +45,15 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
+// BRE_RMW_MAX_RUNS: exact-stage batches with more runs than this accumulate by LDS atomics
+#ifndef BRE_RMW_MAX_RUNS
+#define BRE_RMW_MAX_RUNS 8
+#endif
+// BRE_NODE_RELOAD 1: the production instantiation re-reads o, tmax, 1/d from the SegRec at each node
+// visit (register budget); 0 keeps them in registers
+#ifndef BRE_NODE_RELOAD
+#define BRE_NODE_RELOAD 1
+#endif
 // BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
 #ifndef BRE_BOX_REJECT
 #define BRE_BOX_REJECT 1
@@ -436,6 +445,17 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     if (cm == 0ull) return;
     const int prev = __shfl_up(e.beam, 1);
     unsigned long long starts = __ballot(lane == 0 || e.beam != prev);
+    if (__popcll(starts) > BRE_RMW_MAX_RUNS) {
+        // many short runs (incoherent packets): one LDS float atomic per channel instead; lanes with
+        // the same address resolve in lane order, the same queue-order sum
+        if (contrib) {
+            atomicAdd(&sh.acc[sl].x, v.x);
+            atomicAdd(&sh.acc[sl].y, v.y);
+            atomicAdd(&sh.acc[sl].z, v.z);
+            atomicAdd(&sh.acc[sl].w, v.w);
+        }
+        return;
+    }
     while (starts != 0ull) {
         const int s0 = __ffsll((long long)starts) - 1;
         starts &= starts - 1ull;
@@ -650,7 +670,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int32_t c0 = n.c0, c1 = n.c1;
             f3 lo = L.o, li = L.invs;
             float lt = L.tmax;
-            if (!COUNT) {
+            if (!COUNT && BRE_NODE_RELOAD) {
                 // an opaque copy of the index per visit: keeps the compiler from hoisting the two
                 // loads out of the loop (and the 7 values back into registers)
                 int mi = my;
@@ -975,6 +995,10 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {
         BRE_LAUNCH_TILE(false, 1);
+    } else if (a.occupancy == 4) {
+        BRE_LAUNCH_TILE(false, 4);
+    } else if (a.occupancy == 5) {
+        BRE_LAUNCH_TILE(false, 5);
     } else if (a.occupancy == 6) {
         BRE_LAUNCH_TILE(false, 6);
     } else if (a.occupancy == 8) {
