@@ -34,7 +34,7 @@ static_assert(sizeof(Node) == 64, "Node must be one 64-B line");
 constexpr int32_t kEmptyChild = INT32_MIN;
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
-constexpr int kMaxSplit = 64;          // max work roots (subtrees) per gather
+constexpr int kMaxSplit = 256;         // max work roots (subtrees) per gather
 
 // DevCounters::flags bits.  The host reads the word at every synchronising call and turns a set bit
 // into an error (bre_api.hip: check_flags), whatever the counters option.
