@@ -89,6 +89,8 @@ def parse(argv=None):
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
                     help="synthetic: camera primary segments or incoherent bounce segments")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--progress", action="store_true",
+                    help="print a line per timed step to stderr (synchronises each step; long C4/C5 runs)")
     a = ap.parse_args(argv)
     preset = WORKLOADS[a.workload]
     for k in ("steps", "photons", "width", "height"):
@@ -202,6 +204,10 @@ def main():
     nseg_local = 0
     for k in range(args.steps):
         nseg_local += wl.step(k, events[k], scratch=False)
+        if args.progress:
+            torch.cuda.synchronize(dev)
+            print(f"bench.py: rank {rank} step {k + 1}/{args.steps} done at {time.perf_counter() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
         if k == args.steps - 1 and strong:
             frame.gather_to_root(0)  # one RCCL gather per written image (no-op at N=1)
     torch.cuda.synchronize(dev)
