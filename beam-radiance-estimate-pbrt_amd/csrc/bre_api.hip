@@ -61,7 +61,8 @@ struct bre_ctx {
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
     int block_map = 1;       // internal: tile kernel block mapping (GatherArgs::block_map): 1 rotated
-    int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 measured best (r2, per-run RMW build)
+    int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
+    int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best (r2, no-SLP build: 71 VGPRs)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
@@ -397,6 +398,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.prefilter = c->prefilter;
     a.occupancy = c->occupancy;
     a.block_map = c->block_map;
+    a.tscan = c->tscan;
     a.stack_cap = c->stack_cap;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
@@ -582,6 +584,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated (sweeps)
         if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0, 1 or 2");
         c->block_map = (int)value;
+        return BRE_OK;
+    case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)
+        if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
+        c->tscan = (int)value;
         return BRE_OK;
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }

@@ -140,6 +140,7 @@ struct GatherArgs {
     int occupancy;         // tile kernel register budget: min waves per SIMD (1, 6, 7 or 8)
     int stack_cap;         // traversal stack entries to use (0 = all); tests force an overflow
     int block_map;         // tile kernel block -> (packet, subtree) mapping (k_gather_tile)
+    int tscan;             // tile kernel: transposed scan when on-lanes * 8 < kept beams * tscan (0: off)
 };
 
 // capsule-chunk index (bre_chunk.hip)

@@ -174,6 +174,7 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
     return v;
 }
+__device__ __forceinline__ float readlane_f(float v, int i) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i)); }
 __device__ __forceinline__ float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
 // The whole packet's bundle, wave-uniform (kept in SGPRs).  All lanes must call.
@@ -347,23 +348,37 @@ __device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j
     return B;
 }
 
-// The per-(lane, beam) prefilter as ONE comparison, so that its ballot is the compare's own lane
-// mask (no mask materialisation, no exec juggling in the queue push).  The pair is rejected iff
-//   nn_lo >= 1e-2  and  tn > (Ab' + Al') * nl          (the separable bound above)
-// and `need` is the complement.  key = tn, or -1 when nn_lo < 1e-2 (or NaN): -1 > thr never holds
-// (thr > 0), so such pairs are kept, as before.  al_eff folds the lane's leaf visit and the
-// prefilter switch into the threshold: -inf for a lane off the leaf's box (thr = -inf: never
-// queued), +inf with the prefilter off (thr = +inf: always queued), Al' otherwise.
-// fma(-c, c, 1.00001) > 0 for unit vectors, so nl is never NaN.
+// The per-(lane, beam) prefilter.  The pair is rejected iff
+//   nn_lo >= 1e-2  and  tn > (Ab' + Al') * |n|          (the separable bound above)
+// and `need` is the complement, ANDed by the caller with the lane's leaf visit.  al_eff is Al', or
+// +inf with the prefilter off (thr = +inf: always queued).
+// BRE_SCAN_SQ 1 (default) compares squares, without the square root of |n|:
+//   reject  <=>  nn_lo >= 1e-2  and  fl(tn * tn) > fl(fl(thr * thr) * u),   u = fl(1.0001 - c^2)
+// This implies tn > thr * |n| for the exact cross product n of the stored unit vectors: by the
+// bracket above |n|^2 <= 1.00001 - c^2, and u >= (1.0001 - c^2)(1 - 2^-24) >= |n|^2 + 8.9e-5; the
+// three roundings are at most 3 * 2^-24 relative, so tn^2 > thr^2 u (1 - 1.8e-7) > thr^2 |n|^2.
+// A rejected pair has |n|^2 >= 0.99999 - c^2 >= 1e-2 (bracket), so |n| > 0.1 and the Eb + El fold
+// above still holds.  No underflow can fake a reject: thr >= Ab' > 1.2e-5 and u > 8.9e-5 keep the
+// right side >= 1e-14; an overflowing tn^2 really exceeds a finite right side.  NaN compares keep
+// the pair; +inf thresholds never reject.  (The square-root form, nl = sqrt(1.00001 - c^2) *
+// 1.000001 + 1e-6 >= |n|, is kept as BRE_SCAN_SQ 0.)
+#ifndef BRE_SCAN_SQ
+#define BRE_SCAN_SQ 1
+#endif
 __device__ __forceinline__ bool scan_need(const ScanLane &S, float al_eff, f3 au, const ScanBeam &B) {
     const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
     const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
     const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
-    const float tn =
-        fabsf(__builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x))));
+    const float t = __builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x)));
+    const float thr = B.ab + al_eff;
+    if (BRE_SCAN_SQ) {
+        const float u = __builtin_fmaf(-c, c, 1.0001f);
+        const bool far = (t * t) > (thr * thr) * u;
+        return !((nn_lo >= 1e-2f) & far);
+    }
     const float nl = __builtin_amdgcn_sqrtf(__builtin_fmaf(-c, c, 1.00001f)) * 1.000001f + 1e-6f;
-    const float key = (nn_lo >= 1e-2f) ? tn : -1.0f;
-    return !(key > (B.ab + al_eff) * nl);
+    const float key = (nn_lo >= 1e-2f) ? fabsf(t) : -1.0f;
+    return !(key > thr * nl);
 }
 
 constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
@@ -483,7 +498,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter, int map) {
+    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
     // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
@@ -564,7 +579,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
 
     // scan one leaf tile (<= 64 beams): lane j stages beam j's scan values in LDS; bundle rejects;
     // per lane the separable prefilter on the kept beams; survivors queue for the exact stage
-    const auto leaf = [&](int32_t c, bool lane_on) {
+    const auto leaf = [&](int32_t c, unsigned long long onm) {
+        const bool lane_on = ((onm >> lane) & 1ull) != 0ull;
         const int64_t first = (int64_t)(~c) * leaf_size;
         const int nb = (int)min((int64_t)leaf_size, nvalid - first);
         if (COUNT) {
@@ -594,15 +610,15 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
         }
         __builtin_amdgcn_wave_barrier();
-        // the lane's threshold term for this tile (see scan_need)
-        const float al_eff = !lane_on ? -INFINITY : (prefilter ? SL.al : INFINITY);
+        // the lane's threshold term (see scan_need)
+        const float al_eff = prefilter ? SL.al : INFINITY;
         if (COUNT) {
             pf.useful += __popcll(km);
             // every beam of the tile: the reference box test (candidates) and the pairs the
             // prefilters drop; the queue gets exactly the production survivors, in order
             for (int j = 0; j < nb; ++j) {
                 const bool kept = (km >> j) & 1ull;
-                const bool need = kept && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
+                const bool need = kept && lane_on && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
                 const Box6 box = load_beam(recs, first + j).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
@@ -617,8 +633,40 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const unsigned long long l1 = phase_clock();
         if (BRE_PHASE_TIMING) ph_stage += l1 - l0;
         const unsigned long long ex0 = ph_exact;
-        // two kept beams per step: independent reads and prefilters (ILP, packed by the compiler), then
-        // the survivors are queued beam by beam in order
+        // Few lanes on the tile and many kept beams: the TRANSPOSED scan, one on-lane segment per step
+        // against all kept beams at once (lane j: beam j), so a tile costs min(on lanes, kept beams)
+        // steps.  Segment i's pairs are queued in beam order, exactly the order the beam-major scan
+        // gives them, and every sum is a per-segment sum in queue order: bit-identical results.  The
+        // batches then hold one-pair runs (one beam each), so the exact stage accumulates them by its
+        // LDS-atomic path (or per run), both in queue order.
+        if (tscan > 0 && __popcll(onm) * 8 < __popcll(km) * tscan) {
+            unsigned long long rest = onm;
+            const bool mine = ((km >> lane) & 1ull) != 0ull;
+            while (rest != 0ull) {
+                const int i = __ffsll((long long)rest) - 1;
+                rest &= rest - 1ull;
+                ScanLane Si;
+                Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i),
+                          readlane_f(SL.q.z, i));
+                Si.al = 0.f;
+                const float ali = readlane_f(al_eff, i);
+                const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i),
+                                  readlane_f(L.au.z, i));
+                const bool need = mine && scan_need(Si, ali, aui, scan_beam_lds(sh.tile, lane));
+                const unsigned long long m = __ballot(need);
+                if (m != 0ull) {
+                    const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
+                    sh.q[need ? rank : kQueueCap + lane] = QEntry{(int32_t)(cur_first + lane), i};
+                    t1 += __popcll(m);
+                    drain();
+                }
+            }
+            if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
+            return;
+        }
+        // two kept beams per step: independent reads and prefilters (ILP), then the survivors are
+        // queued beam by beam in order
         unsigned long long todo = km;
         while (todo != 0ull) {
             const int j1 = __ffsll((long long)todo) - 1;
@@ -627,8 +675,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
             const ScanBeam B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
-            const bool n1 = BRE_ABLATE == 3 ? lane_on && ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1);
-            const bool n2 = BRE_ABLATE == 3 ? lane_on && ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2);
+            const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1));
+            const bool n2 = lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2));
             push(j1, n1);
             if (two) push(j2, n2);
             drain();
@@ -656,7 +704,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
 #pragma nounroll
             for (int i = 0; i < 2; ++i) {
                 const unsigned long long m = i ? lm1 : lm0;
-                if (m != 0ull) leaf(i ? lc1 : lc0, ((m >> lane) & 1ull) != 0ull);
+                if (m != 0ull) leaf(i ? lc1 : lc0, m);
             }
             lm0 = lm1 = 0ull;
             if (!have_node) {
@@ -990,7 +1038,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map)
+                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

@@ -81,6 +81,7 @@ def parse(argv=None):
     ap.add_argument("--tile-leaf", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -175,6 +176,8 @@ def main():
         g.set_option(107, args.block_map)
     if args.sort_key >= 0:
         g.set_option(105, args.sort_key)
+    if args.tscan >= 0:
+        g.set_option(108, args.tscan)
     # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
     # are recorded on the stream the kernel runs on
     stream = torch.cuda.Stream(dev)

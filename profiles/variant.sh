@@ -9,7 +9,7 @@ V=$CS/build/variants
 NAME=$1
 DEFS=$2
 mkdir -p "$V"
-FLAGS="-std=c++17 -O3 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math -I$CS -I$HERE/include"
+FLAGS="-std=c++17 -O3 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math ${VARIANT_FLAGS:--fno-slp-vectorize} -I$CS -I$HERE/include"
 /opt/rocm/bin/hipcc $FLAGS $DEFS -c "$CS/bre_gather.hip" -o "$V/bre_gather_$NAME.o" || exit 1
 objs=$(ls "$CS"/build/*.o | grep -v bre_gather.o)
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$V/libbre_$NAME.so" "$V/bre_gather_$NAME.o" $objs || exit 1
