@@ -61,6 +61,14 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
 #endif
+// BRE_SCAN_STATS 1 (profiling builds only): the production tile kernel adds, per wave, scan-shape
+// sums into the counter block instead (profiles/scan_stats.py): lanes on the tile (candidates), kept
+// beams (contributions), scan steps taken (node_visits), steps of a full (lane, beam) pair
+// compaction ceil(on * kept / 64) (leaf_visits), leaf visits (beam_evals), queued pairs
+// (useful_beam_evals), min(on, kept) (prefilter_rejects), transposed tiles (ccp_wave_evals)
+#ifndef BRE_SCAN_STATS
+#define BRE_SCAN_STATS 0
+#endif
 __device__ __forceinline__ unsigned long long phase_clock() {
     return BRE_PHASE_TIMING ? (unsigned long long)__builtin_amdgcn_s_memtime() : 0ull;
 }
@@ -348,37 +356,30 @@ __device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j
     return B;
 }
 
-// The per-(lane, beam) prefilter.  The pair is rejected iff
+// The per-(lane, beam) prefilter as ONE comparison, so that its ballot is the compare's own lane
+// mask (no mask materialisation, no exec juggling in the queue push).  The pair is rejected iff
 //   nn_lo >= 1e-2  and  tn > (Ab' + Al') * |n|          (the separable bound above)
-// and `need` is the complement, ANDed by the caller with the lane's leaf visit.  al_eff is Al', or
-// +inf with the prefilter off (thr = +inf: always queued).
-// BRE_SCAN_SQ 1 (default) compares squares, without the square root of |n|:
-//   reject  <=>  nn_lo >= 1e-2  and  fl(tn * tn) > fl(fl(thr * thr) * u),   u = fl(1.0001 - c^2)
-// This implies tn > thr * |n| for the exact cross product n of the stored unit vectors: by the
-// bracket above |n|^2 <= 1.00001 - c^2, and u >= (1.0001 - c^2)(1 - 2^-24) >= |n|^2 + 8.9e-5; the
-// three roundings are at most 3 * 2^-24 relative, so tn^2 > thr^2 u (1 - 1.8e-7) > thr^2 |n|^2.
+// and `need` is the complement.  Squares, no square root of |n|:
+//   reject  <=>  fl(tn * tn) > fl(fl(thr * |thr|) * u'),   thr = Ab' + al_eff,
+//                u' = fl(1.0001 - c^2) if nn_lo >= 1e-2, else +inf.
+// For thr > 0 this implies tn > thr * |n| for the exact cross product n of the stored unit vectors:
+// by the bracket above |n|^2 <= 1.00001 - c^2, and u' >= (1.0001 - c^2)(1 - 2^-24) >= |n|^2 + 8.9e-5;
+// the three roundings are at most 3 * 2^-24 relative, so tn^2 > thr^2 u' (1 - 1.8e-7) > thr^2 |n|^2.
 // A rejected pair has |n|^2 >= 0.99999 - c^2 >= 1e-2 (bracket), so |n| > 0.1 and the Eb + El fold
-// above still holds.  No underflow can fake a reject: thr >= Ab' > 1.2e-5 and u > 8.9e-5 keep the
-// right side >= 1e-14; an overflowing tn^2 really exceeds a finite right side.  NaN compares keep
-// the pair; +inf thresholds never reject.  (The square-root form, nl = sqrt(1.00001 - c^2) *
-// 1.000001 + 1e-6 >= |n|, is kept as BRE_SCAN_SQ 0.)
-#ifndef BRE_SCAN_SQ
-#define BRE_SCAN_SQ 1
-#endif
+// above still holds.  No underflow can fake a reject: thr >= Ab' > 1.2e-5 and u' > 8.9e-5 keep the
+// right side >= 1e-14; an overflowing tn^2 really exceeds a finite right side; NaN compares keep the
+// pair.  The sign of thr carries two switches: al_eff = FLT_MAX (prefilter off) overflows
+// thr * |thr| to +inf, never a reject; thr = -inf (al_eff = -inf for a lane off the tile, or Ab' =
+// -inf staged for a beam the packet rejects / past the tile's end) makes the right side -inf, always
+// a reject (tn^2 is finite: the lanes and beams involved have finite coordinates).
 __device__ __forceinline__ bool scan_need(const ScanLane &S, float al_eff, f3 au, const ScanBeam &B) {
     const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
     const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
+    const float u = (nn_lo >= 1e-2f) ? __builtin_fmaf(-c, c, 1.0001f) : INFINITY;
     const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
     const float t = __builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x)));
     const float thr = B.ab + al_eff;
-    if (BRE_SCAN_SQ) {
-        const float u = __builtin_fmaf(-c, c, 1.0001f);
-        const bool far = (t * t) > (thr * thr) * u;
-        return !((nn_lo >= 1e-2f) & far);
-    }
-    const float nl = __builtin_amdgcn_sqrtf(__builtin_fmaf(-c, c, 1.00001f)) * 1.000001f + 1e-6f;
-    const float key = (nn_lo >= 1e-2f) ? fabsf(t) : -1.0f;
-    return !(key > thr * nl);
+    return !((t * t) > (thr * fabsf(thr)) * u);
 }
 
 constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
@@ -540,17 +541,20 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int t1 = 0;                // wave-uniform queue length: survivors in q[0, t1)
     int64_t cur_first = 0;     // first beam of the current leaf
     unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
+    unsigned long long ss_on = 0, ss_kept = 0, ss_steps = 0, ss_pairs = 0, ss_leaves = 0, ss_q = 0, ss_min = 0,
+                       ss_tr = 0;
     const unsigned long long ph_t0 = phase_clock();
 
     // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
     // stores (branch-free), a lane that queues nothing into its own discard slot
-    const auto push = [&](int j, bool need) {
+    const auto push = [&](bool need, int32_t e_beam, int32_t e_lane) {
         const unsigned long long m = __ballot(need);
         if (m == 0ull) return;
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
-        sh.q[need ? rank : kQueueCap + lane] = QEntry{(int32_t)(cur_first + j), lane};
+        sh.q[need ? rank : kQueueCap + lane] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
+        if (BRE_SCAN_STATS) ss_q += __popcll(m);
     };
     // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan),
     // then move the < 64 left over to the front of the queue
@@ -605,27 +609,29 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
         __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
-        if (lane < nb) {
-            sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, T.ab);
-            sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
-        }
+        // every lane writes (the transposed scan reads record `lane`): Ab' = -inf for a beam the packet
+        // rejects or past the tile's end (bu = m0 = 0), which scan_need always rejects
+        sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, keep ? T.ab : -INFINITY);
+        sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
         __builtin_amdgcn_wave_barrier();
-        // the lane's threshold term (see scan_need)
-        const float al_eff = prefilter ? SL.al : INFINITY;
+        // the lane's threshold term (see scan_need): Al', FLT_MAX with the prefilter off (never a
+        // reject), -inf for a lane off the tile (always a reject)
+        const float al_on = prefilter ? SL.al : FLT_MAX;
+        const float al_eff = lane_on ? al_on : -INFINITY;
         if (COUNT) {
             pf.useful += __popcll(km);
             // every beam of the tile: the reference box test (candidates) and the pairs the
             // prefilters drop; the queue gets exactly the production survivors, in order
             for (int j = 0; j < nb; ++j) {
                 const bool kept = (km >> j) & 1ull;
-                const bool need = kept && lane_on && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
+                const bool need = kept && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
                 const Box6 box = load_beam(recs, first + j).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                 if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
                 cand += hit;
                 pf.rejects += hit & !need;
-                if (kept) push(j, need);
+                if (kept) push(need, (int32_t)(cur_first + j), lane);
                 drain();
             }
             return;
@@ -639,28 +645,30 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // gives them, and every sum is a per-segment sum in queue order: bit-identical results.  The
         // batches then hold one-pair runs (one beam each), so the exact stage accumulates them by its
         // LDS-atomic path (or per run), both in queue order.
-        if (tscan > 0 && __popcll(onm) * 8 < __popcll(km) * tscan) {
+        const bool transposed = tscan > 0 && __popcll(onm) * 8 < __popcll(km) * tscan;
+        if (BRE_SCAN_STATS) {
+            const unsigned long long on = __popcll(onm), kp = __popcll(km);
+            ss_on += on;
+            ss_kept += kp;
+            ss_steps += transposed ? on : (kp + 1) / 2;
+            ss_pairs += (on * kp + 63) / 64;
+            ss_min += on < kp ? on : kp;
+            ss_tr += transposed;
+            ++ss_leaves;
+        }
+        if (transposed) {
+            // lane j: beam j (Ab' = -inf staged for a beam the packet rejects), segment i on the tile
             unsigned long long rest = onm;
-            const bool mine = ((km >> lane) & 1ull) != 0ull;
             while (rest != 0ull) {
                 const int i = __ffsll((long long)rest) - 1;
                 rest &= rest - 1ull;
                 ScanLane Si;
-                Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i),
-                          readlane_f(SL.q.z, i));
+                Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i), readlane_f(SL.q.z, i));
                 Si.al = 0.f;
-                const float ali = readlane_f(al_eff, i);
-                const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i),
-                                  readlane_f(L.au.z, i));
-                const bool need = mine && scan_need(Si, ali, aui, scan_beam_lds(sh.tile, lane));
-                const unsigned long long m = __ballot(need);
-                if (m != 0ull) {
-                    const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
-                    sh.q[need ? rank : kQueueCap + lane] = QEntry{(int32_t)(cur_first + lane), i};
-                    t1 += __popcll(m);
-                    drain();
-                }
+                const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i), readlane_f(L.au.z, i));
+                const bool need = scan_need(Si, readlane_f(al_on, i), aui, scan_beam_lds(sh.tile, lane));
+                push(need, (int32_t)(cur_first + lane), i);
+                drain();
             }
             if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
             return;
@@ -675,10 +683,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
             const ScanBeam B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
-            const bool n1 = lane_on && (BRE_ABLATE == 3 ? ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1));
-            const bool n2 = lane_on && (BRE_ABLATE == 3 ? ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2));
-            push(j1, n1);
-            if (two) push(j2, n2);
+            const bool n1 = BRE_ABLATE == 3 ? lane_on && ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1);
+            const bool n2 = BRE_ABLATE == 3 ? lane_on && ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2);
+            push(n1, (int32_t)(cur_first + j1), lane);
+            if (two) push(n2, (int32_t)(cur_first + j2), lane);
             drain();
         }
         if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
@@ -791,6 +799,16 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pcnt[2 * ((int64_t)sub * nseg + s)] = COUNT ? cand : -1;
             pcnt[2 * ((int64_t)sub * nseg + s) + 1] = (int32_t)a.w;
         }
+    }
+    if (BRE_SCAN_STATS && !COUNT && lane == 0) {
+        atomicAdd(&ctr->candidates, ss_on);
+        atomicAdd(&ctr->contributions, ss_kept);
+        atomicAdd(&ctr->node_visits, ss_steps);
+        atomicAdd(&ctr->leaf_visits, ss_pairs);
+        atomicAdd(&ctr->beam_evals, ss_leaves);
+        atomicAdd(&ctr->useful_beam_evals, ss_q);
+        atomicAdd(&ctr->prefilter_rejects, ss_min);
+        atomicAdd(&ctr->ccp_wave_evals, ss_tr);
     }
     if (BRE_PHASE_TIMING && !COUNT && lane == 0) {
         atomicAdd(&ctr->candidates, ph_stage);
