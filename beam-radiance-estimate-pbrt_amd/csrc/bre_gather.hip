@@ -55,6 +55,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #define BRE_NODE_RELOAD 1
 #endif
 // BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
+// BRE_NODE_PREFETCH 1: the traversal requests the next node's record before scanning the pending leaves
+// (measured: no gain, SGPR spills at occupancy 7; profiles/r2/explore/explore22)
+#ifndef BRE_NODE_PREFETCH
+#define BRE_NODE_PREFETCH 0
+#endif
 #ifndef BRE_BOX_REJECT
 #define BRE_BOX_REJECT 1
 #endif
@@ -709,19 +714,36 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         }
         int sp = 0;
         while (true) {
+            // The next node is fixed, and its record requested, BEFORE the pending leaves are scanned
+            // (BRE_NODE_PREFETCH): the record's load latency overlaps the leaf scans.
+            bool more = have_node;
+            if (BRE_NODE_PREFETCH && !have_node && sp > 0) {
+                --sp;
+                node = sh.stk[sp];
+                more = true;
+            }
+            NodeV n{};
+            if (BRE_NODE_PREFETCH && more) {
+                node = __builtin_amdgcn_readfirstlane(node);
+                n = load_node(nodes, node);
+            }
 #pragma nounroll
             for (int i = 0; i < 2; ++i) {
                 const unsigned long long m = i ? lm1 : lm0;
                 if (m != 0ull) leaf(i ? lc1 : lc0, m);
             }
             lm0 = lm1 = 0ull;
-            if (!have_node) {
-                if (sp == 0) break;
-                --sp;
-                node = sh.stk[sp];
+            if (BRE_NODE_PREFETCH) {
+                if (!more) break;
+            } else {
+                if (!have_node) {
+                    if (sp == 0) break;
+                    --sp;
+                    node = sh.stk[sp];
+                }
+                node = __builtin_amdgcn_readfirstlane(node);
+                n = load_node(nodes, node);
             }
-            node = __builtin_amdgcn_readfirstlane(node);
-            const NodeV n = load_node(nodes, node);
             if (COUNT) ++visits;
             const int32_t c0 = n.c0, c1 = n.c1;
             f3 lo = L.o, li = L.invs;

@@ -42,7 +42,8 @@ const char *bre_pbrt_messages(const bre_pbrt *p, int32_t *n_errors, int32_t *n_w
    parsed scene and stays valid until bre_pbrt_free. */
 bre_status bre_pbrt_get_scene(const bre_pbrt *p, bre_scene *out);
 /* CreatePhotonBeamIntegrator's parameters for the film of the scene (quick != 0 is pbrt's
-   --quick); *write_frequency (may be NULL) receives "imagewritefrequency" (<= 0: at the end). */
+   --quick); *write_frequency (may be NULL) receives "imagewritefrequency" as given (default 1 << 31 =
+   INT32_MIN, never periodic; bre_render_progressive applies the reference's (iter + 1) % k test). */
 bre_status bre_pbrt_get_render_params(const bre_pbrt *p, int32_t quick, bre_render_params *out,
                                       int32_t *write_frequency);
 /* Film "image" resolution, scale and output file name (NUL-terminated, truncated to cap). */
