@@ -421,7 +421,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         a.roots = c->roots.as<int32_t>();
         a.partial = c->partial.as<float>();
-        HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)nseg));
+        HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)((nseg + 63) / 64 * 64)));  // whole packets
         a.segrec = c->segrec.as<SegRec>();
         if (c->counters || seg_counts) {
             HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));

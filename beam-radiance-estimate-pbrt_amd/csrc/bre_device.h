@@ -103,7 +103,10 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s);
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 
-// One gathered segment as the tile kernel's exact stage reads it (k_seg_prep): 64 B, one line.
+// One gathered segment as the tile kernel's exact stage reads it (k_seg_prep): 64 B as four 16-B
+// planes.  In HBM the records are stored PLANE-MAJOR PER PACKET of 64 segments (seg_plane): plane k of
+// the packet's 64 segments is one contiguous 1 KB run, so an exact-stage load of plane k for 64
+// arbitrary lanes of the packet touches at most 1 KB (16 lines) instead of 64 separate lines.
 struct alignas(16) SegRec {
     float o[3], tmax;   // ray.o, ray.tMax
     float p[3], mag_a;  // isect.p, |p - o|
@@ -113,6 +116,10 @@ struct alignas(16) SegRec {
     float omax;         // max |o_i| + |p - o|
 };
 static_assert(sizeof(SegRec) == 64, "SegRec must be one 64-B line");
+// plane k (0..3) of segment s in the packet-plane layout (buffers hold ceil(nseg / 64) * 64 records)
+__device__ __forceinline__ const float4 *seg_plane(const SegRec *base, int64_t s, int k) {
+    return reinterpret_cast<const float4 *>(base) + ((s >> 6) << 8) + (k << 6) + (s & 63);
+}
 
 struct GatherArgs {
     int64_t nseg;

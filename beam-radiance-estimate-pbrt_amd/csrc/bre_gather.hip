@@ -417,10 +417,10 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const int64_t b = e.beam;
     // every load of the pair is issued at once (one memory round trip per batch; most queued pairs
     // pass the box test, so the second half is rarely wasted)
-    const float4 *sr = reinterpret_cast<const float4 *>(srec + seg0 + sl);
+    const float4 *sr = seg_plane(srec, seg0 + sl, 0);  // packet-plane layout: plane k at sr[64 k]
     const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
-    const float4 s0 = sr[0], s3 = sr[3], bx = rb[0], by = rb[1];
-    const float4 s1 = sr[1], s2 = sr[2], bz = rb[2], bw = rb[3];
+    const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
+    const float4 s1 = sr[64], s2 = sr[128], bz = rb[2], bw = rb[3];
     const float4 pv = pw[b];
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
@@ -753,8 +753,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 // loads out of the loop (and the 7 values back into registers)
                 int mi = my;
                 asm volatile("" : "+v"(mi));
-                const float4 *mp = reinterpret_cast<const float4 *>(srec + mi);
-                const float4 a0 = mp[0], a3 = mp[3];
+                const float4 *mp = seg_plane(srec, mi, 0);
+                const float4 a0 = mp[0], a3 = mp[192];
                 lo = mk(a0.x, a0.y, a0.z);
                 lt = a0.w;
                 li = mk(a3.x, a3.y, a3.z);
@@ -853,8 +853,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     }
 }
 
-// One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec): the values
-// load_lane derives, computed once per gather instead of once per (packet, subtree) wave.
+// One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec, packet-plane
+// layout): the values load_lane derives, computed once per gather instead of once per (packet,
+// subtree) wave.
 __global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__restrict__ so,
                                                   const float *__restrict__ sp_, const float *__restrict__ sd,
                                                   const float *__restrict__ stmax, SegRec *__restrict__ out) {
@@ -862,11 +863,11 @@ __global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__r
     if (s >= nseg) return;
     Lane L;
     load_lane(s, nseg, so, sp_, sd, stmax, L);
-    float4 *q = reinterpret_cast<float4 *>(out + s);
+    float4 *q = const_cast<float4 *>(seg_plane(out, s, 0));  // packet-plane layout (bre_device.h)
     q[0] = make_float4(L.o.x, L.o.y, L.o.z, L.tmax);
-    q[1] = make_float4(L.p.x, L.p.y, L.p.z, L.mag_a);
-    q[2] = make_float4(L.au.x, L.au.y, L.au.z, __int_as_float(L.has_inf ? 1 : 0));
-    q[3] = make_float4(L.invs.x, L.invs.y, L.invs.z, L.omax);
+    q[64] = make_float4(L.p.x, L.p.y, L.p.z, L.mag_a);
+    q[128] = make_float4(L.au.x, L.au.y, L.au.z, __int_as_float(L.has_inf ? 1 : 0));
+    q[192] = make_float4(L.invs.x, L.invs.y, L.invs.z, L.omax);
 }
 
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the
