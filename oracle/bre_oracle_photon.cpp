@@ -116,6 +116,7 @@ static void TraceRecursive(Ray photonRay, int depth, Spectrum beta, Sampler &sam
 // Emission (photonbeam.cpp:383-421): the light by power (lightDistr->SampleDiscrete), then
 // DiffuseAreaLight::Sample_Le (diffuse.cpp:89-123) on its triangle (Triangle::Sample)
 static void TracePhoton(const Scene &sc, uint64_t seq, int MaxDepth, Float BeamRadius, std::vector<Beam> &out) {
+    if (sc.lights.empty()) return;  // no light to shoot from (libbre rejects such scenes)
     Sampler sampler(seq);
     Float lightPdf;
     const int lightNum = SampleDiscrete(sc, sampler.Get1D(), &lightPdf);
@@ -305,6 +306,56 @@ void ora_grid_eval(const bre_scene *scene, int32_t kind, int64_t n, const float 
         }
         if (draws) draws[i] = cs.n;
     }
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Test support: the reference's own shape and sampling tests (src/tests/shapes.cpp,
+// src/tests/sampling.cpp) restated on the oracle's pbrt primitives (tests/test_ref_tests.py).
+
+// For n rays (o, d, tMax = +inf): how many of the scene's triangles Triangle::Intersect hits
+// (Triangle.Watertight, shapes.cpp:28-152, requires >= 1 from inside a closed mesh)
+void ora_tri_hits(const bre_scene *scene, int64_t n, const float *o, const float *d, int32_t *hits) {
+    orp::Scene sc = orp::make_scene(scene);
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t k = 0;
+        for (const orp::Tri &T : sc.tris) {
+            orp::Ray r;
+            r.o = orp::V3(o + 3 * i);
+            r.d = orp::V3(d + 3 * i);
+            r.tMax = orp::Infinity;
+            orp::Float t;
+            orp::Isect is;
+            k += orp::IntersectTri(T, r, &t, &is) ? 1 : 0;
+        }
+        hits[i] = k;
+    }
+}
+
+// Triangle::Sample(u) (triangle.cpp:543-568, area measure) of triangle `tri` for n sample pairs
+void ora_tri_sample(const bre_scene *scene, int32_t tri, int64_t n, const float *u, float *p, float *nrm,
+                    float *pdf) {
+    orp::Scene sc = orp::make_scene(scene);
+    const orp::Tri &T = sc.tris[tri];
+    for (int64_t i = 0; i < n; ++i) {
+        const orp::ShapeSample s = orp::SampleTri(T, u[2 * i], u[2 * i + 1]);
+        for (int k = 0; k < 3; ++k) {
+            p[3 * i + k] = s.p[k];
+            nrm[3 * i + k] = s.n[k];
+        }
+        pdf[i] = s.pdf;
+    }
+}
+
+// Distribution1D(func, nf) (sampling.h:55-100): SampleDiscrete for m values of u (index, pdf,
+// uRemapped) and DiscretePDF of every entry (Distribution1D.Discrete, sampling.cpp:231-280)
+void ora_distribution1d(const float *func, int32_t nf, int64_t m, const float *u, int32_t *idx, float *pdf,
+                        float *urem, float *dpdf) {
+    const orp::Distribution1D dist(func, nf);
+    for (int64_t i = 0; i < m; ++i) idx[i] = dist.SampleDiscrete(u[i], &pdf[i], &urem[i]);
+    for (int i = 0; i < nf; ++i) dpdf[i] = dist.DiscretePDF(i);
 }
 
 }  // extern "C"

@@ -246,12 +246,48 @@ struct Tri {
     bool emit;
 };
 
+// Distribution1D, sampling.h:55-100: the piecewise-constant CDF of func (the constructor) and
+// SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389)
+struct Distribution1D {
+    std::vector<Float> func, cdf;
+    Float funcInt = 0;
+    Distribution1D() = default;
+    Distribution1D(const Float *f, int n) : func(f, f + n), cdf(n + 1) {
+        cdf[0] = 0;
+        for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] / (Float)n;
+        funcInt = cdf[n];
+        if (funcInt == 0) {
+            for (int i = 1; i < n + 1; ++i) cdf[i] = Float(i) / Float(n);
+        } else {
+            for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+        }
+    }
+    int Count() const { return (int)func.size(); }
+    int SampleDiscrete(Float u, Float *pdf, Float *uRemapped = nullptr) const {
+        const int size = (int)cdf.size();
+        int first = 0, len = size;
+        while (len > 0) {
+            int half = len >> 1, middle = first + half;
+            if (cdf[middle] <= u) {
+                first = middle + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        const int offset = std::min(std::max(first - 1, 0), size - 2);  // Clamp(first - 1, 0, size - 2)
+        if (pdf) *pdf = (funcInt > 0) ? func[offset] / (funcInt * (Float)Count()) : 0;
+        if (uRemapped) *uRemapped = (u - cdf[offset]) / (cdf[offset + 1] - cdf[offset]);
+        return offset;
+    }
+    Float DiscretePDF(int index) const { return func[index] / (funcInt * (Float)Count()); }
+};
+
 struct Scene {
     std::vector<Tri> tris;
     std::vector<int> lights;  // scene.lights: the emitting triangles, in triangle order
     // ComputeLightPowerDistribution (integrator.cpp:217-225) -> Distribution1D (sampling.h:55-100)
-    std::vector<Float> lfunc, lcdf;
-    Float lfuncInt = 0;
+    Distribution1D ldist;
     bool medium;
     Spectrum sigma_t, sigma_s;
     Float g;
@@ -263,23 +299,8 @@ struct Scene {
     Float gridSigmaT = 0, invMaxDensity = 0;
 };
 
-// Distribution1D::SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389)
-static int SampleDiscrete(const Scene &sc, Float u, Float *pdf) {
-    const int size = (int)sc.lcdf.size();
-    int first = 0, len = size;
-    while (len > 0) {
-        int half = len >> 1, middle = first + half;
-        if (sc.lcdf[middle] <= u) {
-            first = middle + 1;
-            len -= half + 1;
-        } else {
-            len = half;
-        }
-    }
-    const int offset = std::min(std::max(first - 1, 0), size - 2);  // Clamp(first - 1, 0, size - 2)
-    if (pdf) *pdf = (sc.lfuncInt > 0) ? sc.lfunc[offset] / (sc.lfuncInt * (Float)sc.lfunc.size()) : 0;
-    return offset;
-}
+// the light-power distribution's SampleDiscrete (Distribution1D above)
+static int SampleDiscrete(const Scene &sc, Float u, Float *pdf) { return sc.ldist.SampleDiscrete(u, pdf); }
 
 static Scene make_scene(const bre_scene *s) {
     Scene sc;
@@ -309,19 +330,12 @@ static Scene make_scene(const bre_scene *s) {
         sc.tris.push_back(T);
     }
     // DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:53-55), .y()
-    const int n = (int)sc.lights.size();
+    std::vector<Float> lfunc;
     for (int l : sc.lights) {
         const Tri &T = sc.tris[l];
-        sc.lfunc.push_back(((T.Le * (Float)1) * T.area * Pi).y());
+        lfunc.push_back(((T.Le * (Float)1) * T.area * Pi).y());
     }
-    sc.lcdf.assign(n + 1, 0.f);
-    for (int i = 1; i < n + 1; ++i) sc.lcdf[i] = sc.lcdf[i - 1] + sc.lfunc[i - 1] / (Float)n;
-    sc.lfuncInt = sc.lcdf[n];
-    if (sc.lfuncInt == 0) {
-        for (int i = 1; i < n + 1; ++i) sc.lcdf[i] = Float(i) / Float(n);
-    } else {
-        for (int i = 1; i < n + 1; ++i) sc.lcdf[i] /= sc.lfuncInt;
-    }
+    if (!lfunc.empty()) sc.ldist = Distribution1D(lfunc.data(), (int)lfunc.size());
     sc.medium = s->has_medium != 0;
     Spectrum sa(s->sigma_a);
     sc.sigma_s = Spectrum(s->sigma_s);

@@ -61,6 +61,9 @@ class Oracle:
         lib.ora_grid_density.argtypes = [P, I64, P, P]
         lib.ora_set_libm.argtypes = [I32]
         lib.ora_grid_eval.argtypes = [P, I32, I64, P, P, P, U64, P, P]
+        lib.ora_tri_hits.argtypes = [P, I64, P, P, P]
+        lib.ora_tri_sample.argtypes = [P, I32, I64, P, P, P, P]
+        lib.ora_distribution1d.argtypes = [P, I32, I64, P, P, P, P, P]
 
     # -- primitives --
     def set_libm(self, on: bool):
@@ -150,6 +153,31 @@ class Oracle:
         return y
 
     # -- GridDensityMedium (oracle/ora_pbrt.h) --
+    # -- the reference's own shape / sampling tests (tests/test_ref_tests.py) --
+    def tri_hits(self, scene, o, d):
+        """Per ray (tMax = inf): how many of the scene's triangles Triangle::Intersect hits."""
+        o, d = (np.ascontiguousarray(x, np.float32) for x in (o, d))
+        out = np.zeros(o.shape[0], np.int32)
+        self.lib.ora_tri_hits(ctypes.addressof(scene), o.shape[0], _p(o), _p(d), _p(out))
+        return out
+
+    def tri_sample(self, scene, tri, u):
+        """Triangle::Sample(u) of triangle `tri` (area measure): points, normals, pdfs."""
+        u = np.ascontiguousarray(u, np.float32)
+        n = u.shape[0]
+        p, nrm, pdf = np.zeros((n, 3), np.float32), np.zeros((n, 3), np.float32), np.zeros(n, np.float32)
+        self.lib.ora_tri_sample(ctypes.addressof(scene), int(tri), n, _p(u), _p(p), _p(nrm), _p(pdf))
+        return p, nrm, pdf
+
+    def distribution1d(self, func, u):
+        """Distribution1D(func): SampleDiscrete(u) -> (index, pdf, uRemapped), and DiscretePDF."""
+        func, u = np.ascontiguousarray(func, np.float32), np.ascontiguousarray(u, np.float32)
+        m = u.shape[0]
+        idx, pdf, urem = np.zeros(m, np.int32), np.zeros(m, np.float32), np.zeros(m, np.float32)
+        dpdf = np.zeros(func.shape[0], np.float32)
+        self.lib.ora_distribution1d(_p(func), func.shape[0], m, _p(u), _p(idx), _p(pdf), _p(urem), _p(dpdf))
+        return idx, pdf, urem, dpdf
+
     def grid_density(self, scene, p):
         p = np.ascontiguousarray(p, np.float32)
         out = np.zeros(p.shape[0], np.float32)
