@@ -72,7 +72,7 @@ def parse(argv=None):
     ap.add_argument("--max-depth", type=int, default=5)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=1)
-    ap.add_argument("--split", type=int, default=64, help="BVH subtrees (work roots) per segment packet")
+    ap.add_argument("--split", type=int, default=256, help="BVH subtrees (work roots) per segment packet")
     ap.add_argument("--prefilter", type=int, default=1)
     ap.add_argument("--chunk-len", type=int, default=400, help="kernel 5: chunk length in units of E/100")
     ap.add_argument("--chunk-leaf", type=int, default=1, help="kernel 5: chunks per LBVH leaf")
