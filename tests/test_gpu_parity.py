@@ -386,6 +386,32 @@ def test_device_pixel_error_reported_at_synchronize(bre, synth):
         g.synchronize()  # cleared
 
 
+@pytest.mark.parametrize("kind", ["camera", "bounce", "long"])
+def test_transposed_scan_is_bit_identical(bre, synth, kind):
+    """The transposed scan (one on-lane segment per step against all beams of a tile) queues each
+    segment's pairs in the same beam order as the beam-major scan, so forcing it everywhere (threshold
+    64: whenever fewer lanes are on than 8x the kept beams) or never (0) changes no output bit; the
+    default (6) mixes both within one gather."""
+    if kind == "long":
+        beams = synth.fog_beams(6000, seed=81, radius=0.05, mean_length=0.8)
+        segs = synth.bounce_segments(6000, seed=82)
+        R = 0.08
+    else:
+        beams = synth.fog_beams(20000, seed=83)
+        segs = synth.camera_segments(64, 64, seed=84) if kind == "camera" else synth.bounce_segments(4096, seed=85)
+        R = 0.01
+    outs = {}
+    for t in (0, 6, 64):
+        with bre.BeamGather(0, counters=False, kernel=0) as g:
+            g.set_option(108, t)
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            outs[t] = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True)
+    assert outs[0]["counts"][:, 1].sum() > 0
+    for t in (6, 64):
+        assert np.array_equal(outs[t]["seg_rgb"], outs[0]["seg_rgb"]), t
+        assert np.array_equal(outs[t]["counts"][:, 1], outs[0]["counts"][:, 1]), t
+
+
 def test_removed_kernels_are_rejected(bre):
     with bre.BeamGather(0) as g:
         for k in (1, 3, 6, 7):
