@@ -82,6 +82,7 @@ def parse(argv=None):
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--emulate-shard", type=str, default=None, help=argparse.SUPPRESS)  # "R/N": rank R's share on 1 GPU
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -161,7 +162,10 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     strong = args.scaling == "strong"
-    frame = dmod.ShardedFrame(args.width, args.height, rank if strong else 0, world if strong else 1, device=dev)
+    srank, scount = (rank, world) if strong else (0, 1)
+    if args.emulate_shard and world == 1:  # one rank's share of an N-GPU strong-scaling run, on this GPU
+        srank, scount = (int(x) for x in args.emulate_shard.split("/"))
+    frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev)
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
     g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
@@ -185,7 +189,7 @@ def main():
     g.set_stream(stream.cuda_stream)
 
     if args.workload != "synthetic":
-        wl = SceneWorkload(args, bre, g, frame, rank if strong else 0, world if strong else 1)
+        wl = SceneWorkload(args, bre, g, frame, srank, scount)
     else:
         wl = SyntheticWorkload(args, bre, g, frame, dev)
 
