@@ -26,7 +26,7 @@ STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
 OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
-OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS = 11, 12, 13
+OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS, OPT_SHARD_BLOCK = 11, 12, 13, 14
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -184,8 +184,10 @@ class BeamGather:
     def set_option(self, opt: int, value: int):
         self._check(self.lib.bre_set_option(self.h, opt, int(value)))
 
-    def set_shard(self, rank: int, count: int):
-        """Camera pass walks only the 16x16 image tiles t with t % count == rank."""
+    def set_shard(self, rank: int, count: int, block: int = 1):
+        """Camera pass walks only the 16x16 image tiles of the blocks of block x block tiles whose
+        row-major block index is rank (mod count) (dist.tile_pixels lists the same pixels)."""
+        self.set_option(OPT_SHARD_BLOCK, int(block))
         self.set_option(OPT_SHARD_COUNT, int(count))
         self.set_option(OPT_SHARD_RANK, int(rank))
 

@@ -65,6 +65,7 @@ struct bre_ctx {
     int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best (r2, no-SLP build: 71 VGPRs)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
+    int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
@@ -566,6 +567,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
             return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_RANK must be in [0, shard count)");
         c->shard_rank = (int)value;
         return BRE_OK;
+    case BRE_OPT_SHARD_BLOCK:
+        if (value < 1 || value > 4096) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_BLOCK must be in 1..4096");
+        c->shard_block = (int)value;
+        return BRE_OK;
     case BRE_OPT_SHARD_COUNT:
         if (value < 1 || value > 65536) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_COUNT must be in 1..65536");
         c->shard_count = (int)value;
@@ -842,7 +847,8 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->cam_dev.as<DevCamera>(), c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
-                            c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count, c->stream));
+                            c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count, c->shard_block,
+                            c->stream));
     // total = offs[S-1] + valid[S-1]
     HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
     int64_t last_off = 0;

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
                                                      float *__restrict__ sd, float *__restrict__ st,
                                                      int32_t *__restrict__ spix, int32_t *__restrict__ valid,
                                                      float *__restrict__ surface, unsigned int *__restrict__ flags,
-                                                     int shard_rank, int shard_count) {
+                                                     int shard_rank, int shard_count, int shard_block) {
     const DevScene &S = *Sp;
     const DevCamera &C = *Cp;
     const int64_t slot = (int64_t)blockIdx.x * kCamBlock + threadIdx.x;
@@ -408,8 +408,12 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
     for (int dd = 0; dd < max_depth; ++dd) valid[dd * nslots + slot] = 0;
     if (px >= C.width || py >= C.height) return;
     // image-tile sharding: this context walks only the reference's 16x16 camera-pass tiles
-    // (photonbeam.cpp:345-347, 444-452) with tile index = rank (mod count)
-    if (shard_count > 1 && ((py >> 4) * ((C.width + 15) >> 4) + (px >> 4)) % shard_count != shard_rank) return;
+    // (photonbeam.cpp:345-347, 444-452) of the blocks of shard_block x shard_block tiles whose
+    // row-major block index = rank (mod count)
+    if (shard_count > 1) {
+        const int nbx = (((C.width + 15) >> 4) + shard_block - 1) / shard_block;
+        if ((((py >> 4) / shard_block) * nbx + (px >> 4) / shard_block) % shard_count != shard_rank) return;
+    }
     const int pixel = py * C.width + px;
 
     HaltonDev hs{Cp, perms, halton_index(C, px, py, iteration), 0, Pcg{}};
@@ -521,12 +525,13 @@ int64_t camera_slots(int width, int height) {
 
 hipError_t launch_camera(const DevScene *scene, const DevCamera *cam, const uint16_t *perms, int width, int height,
                          int iteration, int max_depth, int render_surfaces, int render_media, const CamSlots &s,
-                         float *surface, unsigned int *flags, int shard_rank, int shard_count, hipStream_t stream) {
+                         float *surface, unsigned int *flags, int shard_rank, int shard_count, int shard_block,
+                         hipStream_t stream) {
     const int64_t nslots = camera_slots(width, height);
     if (nslots == 0) return hipSuccess;
     hipLaunchKernelGGL(k_camera, dim3((unsigned)(nslots / kCamBlock)), dim3(kCamBlock), 0, stream, scene, cam, perms,
                        iteration, max_depth, render_surfaces, render_media, nslots, s.o, s.p, s.d, s.t, s.pix,
-                       s.valid, surface, flags, shard_rank, shard_count);
+                       s.valid, surface, flags, shard_rank, shard_count, shard_block);
     return hipGetLastError();
 }
 

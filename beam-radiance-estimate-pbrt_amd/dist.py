@@ -16,13 +16,18 @@ from __future__ import annotations
 import numpy as np
 
 
-def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16) -> np.ndarray:
-    """Pixel indices (y*w + x) of the tiles owned by `rank`, tile-major, row-major inside a tile."""
+def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16, block: int = 1) -> np.ndarray:
+    """Pixel indices (y*w + x) of the tiles owned by `rank` -- the tiles of the blocks of block x block
+    tiles whose row-major block index is rank (mod world), as libbre's camera pass deals them
+    (BRE_OPT_SHARD_BLOCK) -- tile-major in row-major tile order, row-major inside a tile."""
     ntx = (w + tile - 1) // tile
     nty = (h + tile - 1) // tile
+    nbx = (ntx + block - 1) // block
     out = []
-    for t in range(rank, ntx * nty, world):
+    for t in range(ntx * nty):
         tx, ty = t % ntx, t // ntx
+        if ((ty // block) * nbx + tx // block) % world != rank:
+            continue
         xs = np.arange(tx * tile, min(tx * tile + tile, w))
         ys = np.arange(ty * tile, min(ty * tile + tile, h))
         out.append((ys[:, None] * w + xs[None, :]).ravel())
@@ -32,19 +37,20 @@ def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16) -> np.nda
 class ShardedFrame:
     """Full-resolution RGB accumulation buffer of one rank (only its own tiles are ever written)."""
 
-    def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16):
+    def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16, block: int = 1):
         import torch
 
-        self.w, self.h, self.rank, self.world, self.tile = w, h, rank, world, tile
-        self.pixels = tile_pixels(w, h, rank, world, tile)
+        self.w, self.h, self.rank, self.world, self.tile, self.block = w, h, rank, world, tile, block
+        self.pixels = tile_pixels(w, h, rank, world, tile, block)
         self.accum = torch.zeros((w * h, 3), dtype=torch.float32, device=device)
         self.device = device
         self._band = None
         if world > 1:
-            counts = [tile_pixels(w, h, r, world, tile).shape[0] for r in range(world)]
+            counts = [tile_pixels(w, h, r, world, tile, block).shape[0] for r in range(world)]
             self.band_len = max(counts)
             self._idx = torch.from_numpy(self.pixels).to(device)
-            self._all_idx = [torch.from_numpy(tile_pixels(w, h, r, world, tile)).to(device) for r in range(world)]
+            self._all_idx = [torch.from_numpy(tile_pixels(w, h, r, world, tile, block)).to(device)
+                             for r in range(world)]
 
     @property
     def npix(self) -> int:

@@ -82,6 +82,8 @@ def parse(argv=None):
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--shard-block", type=int, default=1,
+                    help="strong scaling: tiles per side of the image blocks dealt round-robin to the GPUs")
     ap.add_argument("--emulate-shard", type=str, default=None, help=argparse.SUPPRESS)  # "R/N": rank R's share on 1 GPU
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -165,7 +167,7 @@ def main():
     srank, scount = (rank, world) if strong else (0, 1)
     if args.emulate_shard and world == 1:  # one rank's share of an N-GPU strong-scaling run, on this GPU
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
-    frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev)
+    frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block)
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
     g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
@@ -426,7 +428,7 @@ class SceneWorkload:
         else:
             self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
-        g.set_shard(shard_rank, shard_count)
+        g.set_shard(shard_rank, shard_count, frame.block)
         self.ld = frame.accum
         self.scratch = torch.zeros_like(self.ld)
         self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "

@@ -75,8 +75,10 @@ typedef enum bre_option {
     BRE_OPT_SPLIT = 6,       /* kernels 0/4: BVH subtrees per segment packet, power of two 1..256 (default 256) */
     BRE_OPT_PREFILTER = 7,   /* kernels 0/4/5: 0/1 conservative line-distance rejects before the exact
                                 closest-point code (default 1; results are identical either way) */
-    BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles t (the reference's
-                                camera-pass tiles, photonbeam.cpp:345-347) with t % count == rank */
+    BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles (the reference's
+                                camera-pass tiles, photonbeam.cpp:345-347) of the blocks of
+                                BRE_OPT_SHARD_BLOCK^2 tiles whose row-major block index b has
+                                b % count == rank (block 1: tile t with t % count == rank) */
     BRE_OPT_SHARD_COUNT = 9, /* camera pass: number of image-tile shards (default 1 = all tiles).
                                 Set the count before the rank.  Per-pixel results do not depend on
                                 the sharding, so summing the shards' Ld gives the 1-shard image. */
@@ -85,9 +87,12 @@ typedef enum bre_option {
     BRE_OPT_CHUNK_LEN = 11,  /* kernel 5: chunk length in units of E/100, E = (R + r)(1 + 1e-3) + margin
                                 (25..100000, default 400) */
     BRE_OPT_CHUNK_LEAF = 12, /* kernel 5: chunks per LBVH leaf, 1..64 (default 1) */
-    BRE_OPT_SORT_SEGMENTS = 13 /* bre_gather_camera: 0/1 hand the camera-pass segments to the gather
+    BRE_OPT_SORT_SEGMENTS = 13, /* bre_gather_camera: 0/1 hand the camera-pass segments to the gather
                                   in 6-D Morton order of (origin, end point) (default 1); pixel sums
                                   are the same pair contributions either way */
+    BRE_OPT_SHARD_BLOCK = 14 /* camera pass: tiles per side of the blocks dealt to the shards (1..4096,
+                                default 1); larger blocks keep a shard's bounce segments as dense in
+                                space as the whole film's, so its packets stay coherent */
 } bre_option;
 
 typedef struct bre_stats {

@@ -51,8 +51,14 @@ def _render(rank, world, port, outdir):
 def test_tiles_partition_image():
     dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
     for world in (1, 2, 3, 8):
-        allpix = np.concatenate([dmod.tile_pixels(100, 70, r, world) for r in range(world)])
-        assert np.array_equal(np.sort(allpix), np.arange(100 * 70))
+        for block in (1, 2, 4):
+            parts = [dmod.tile_pixels(100, 70, r, world, block=block) for r in range(world)]
+            allpix = np.concatenate(parts)
+            assert np.array_equal(np.sort(allpix), np.arange(100 * 70)), (world, block)
+    # block 2 over 7 x 5 tiles of 16 px: blocks (bx, by) with by * 4 + bx = rank (mod world)
+    p = dmod.tile_pixels(100, 70, 1, 3, block=2)
+    tiles = {(int(x) // 16, int(y) // 16) for x, y in zip(p % 100, p // 100)}
+    assert tiles == {(tx, ty) for tx in range(7) for ty in range(5) if ((ty // 2) * 4 + tx // 2) % 3 == 1}
 
 
 def test_two_rank_gloo_render_equals_single_rank(tmp_path, oracle, synth):

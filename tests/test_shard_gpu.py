@@ -17,8 +17,9 @@ def _rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
-@pytest.mark.parametrize("world,shape,photons", [(4, (256, 192), 200_000), (8, (512, 512), 300_000)])
-def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, photons):
+@pytest.mark.parametrize("world,shape,photons,block", [(4, (256, 192), 200_000, 1), (8, (512, 512), 300_000, 1),
+                                                       (8, (512, 512), 300_000, 4), (3, (200, 136), 100_000, 2)])
+def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, photons, block):
     import torch
 
     dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
@@ -28,7 +29,7 @@ def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, ph
 
     def render(rank, count, frame):
         with bre.BeamGather(0) as g:
-            g.set_shard(rank, count)
+            g.set_shard(rank, count, block)
             g.trace_photons(scene, photons, it, 5, R)
             n = g.camera_pass(scene, W, H, it, 5, True, True, surface=frame.accum)
             g.gather_camera(R, frame.accum)
@@ -37,7 +38,7 @@ def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, ph
 
     ref = dmod.ShardedFrame(W, H, 0, 1, device="cuda")
     n_ref = render(0, 1, ref)
-    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda") for r in range(world)]
+    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda", block=block) for r in range(world)]
     n_sh = sum(render(r, world, f) for r, f in enumerate(frames))
     assert n_sh == n_ref  # the shards partition the camera segments
     owned = np.zeros(W * H, bool)
