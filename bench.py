@@ -217,8 +217,8 @@ def main():
             torch.cuda.synchronize(dev)
             print(f"bench.py: rank {rank} step {k + 1}/{args.steps} done at {time.perf_counter() - t0:.1f} s",
                   file=sys.stderr, flush=True)
-        if k == args.steps - 1 and strong:
-            frame.gather_to_root(0)  # one RCCL gather per written image (no-op at N=1)
+        if k == args.steps - 1 and strong and world > 1:
+            frame.gather_to_root(0)  # one RCCL gather per written image
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
