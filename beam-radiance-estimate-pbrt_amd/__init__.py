@@ -26,7 +26,7 @@ STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE
                 4: "BRE_ERR_STATE", 5: "BRE_ERR_NO_DEVICE"}
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
 OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
-OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS, OPT_SHARD_BLOCK = 11, 12, 13, 14
+OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS, OPT_SHARD_BLOCK, OPT_SHARD_MODE = 11, 12, 13, 14, 15
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -36,7 +36,7 @@ EXPORTS = [
     "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell", "bre_scene_cornell_smoke", "bre_smoke_density",
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
-    "bre_render_progressive",
+    "bre_render_progressive", "bre_shard_segments",
 ]
 
 
@@ -109,6 +109,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = I32
     lib.bre_beam_radius_at.argtypes = [F, F, I32]
     lib.bre_beam_radius_at.restype = F
+    lib.bre_shard_segments.argtypes = [I64, I32, I32]
+    lib.bre_shard_segments.restype = I64
     lib.bre_resolve_image.argtypes = [I64, P, I32, P]
     lib.bre_resolve_image.restype = I32
     lib.bre_trace_photons.argtypes = [P, P, I64, I32, I32, F, ctypes.POINTER(I64)]
@@ -184,9 +186,12 @@ class BeamGather:
     def set_option(self, opt: int, value: int):
         self._check(self.lib.bre_set_option(self.h, opt, int(value)))
 
-    def set_shard(self, rank: int, count: int, block: int = 1):
-        """Camera pass walks only the 16x16 image tiles of the blocks of block x block tiles whose
-        row-major block index is rank (mod count) (dist.tile_pixels lists the same pixels)."""
+    def set_shard(self, rank: int, count: int, block: int = 1, packets: bool = False):
+        """Tile shards (default): the camera pass walks only the 16x16 image tiles of the blocks of
+        block x block tiles whose row-major block index is rank (mod count) (dist.tile_pixels lists the
+        same pixels).  packets=True: the whole camera pass, and the gather of this rank's range of the
+        sorted packets (shard_range); the ranks' films sum to the whole film."""
+        self.set_option(OPT_SHARD_MODE, 1 if packets else 0)
         self.set_option(OPT_SHARD_BLOCK, int(block))
         self.set_option(OPT_SHARD_COUNT, int(count))
         self.set_option(OPT_SHARD_RANK, int(rank))
@@ -323,6 +328,20 @@ class BeamGather:
 
     def __exit__(self, *a):
         self.close()
+
+
+def shard_segments(n_segments: int, rank: int, count: int) -> int:
+    """How many camera segments shard `rank` of `count` gathers in packet mode (libbre)."""
+    return int(load_library().bre_shard_segments(int(n_segments), int(rank), int(count)))
+
+
+def shard_packet_index(n_segments: int, rank: int, count: int):
+    """The segment indices (in the gathered order) of shard `rank`'s packets p = rank (mod count): the
+    host view of libbre's packet pick, for tests and CPU rehearsals."""
+    import numpy as np
+    npk = (int(n_segments) + 63) // 64
+    idx = (np.arange(rank, npk, count, dtype=np.int64)[:, None] * 64 + np.arange(64)[None, :]).ravel()
+    return idx[idx < n_segments]
 
 
 def beam_radius_at(initial_radius: float, alpha: float, iteration: int) -> float:

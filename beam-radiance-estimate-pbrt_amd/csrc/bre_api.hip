@@ -66,6 +66,7 @@ struct bre_ctx {
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
+    int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
@@ -78,6 +79,7 @@ struct bre_ctx {
     // coherence sort of the camera-pass segments before the gather (bre_sort.hip)
     bool sort_segments = true;
     DevMem ss_bounds, ss_keys, ss_keys_alt, ss_vals, ss_vals_alt, ss_tmp, ss_o, ss_p, ss_d, ss_t, ss_pix;
+    DevMem sp_o, sp_p, sp_d, sp_t, sp_pix, sp_index;  // this packet shard's segments (contiguous)
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     int built_leaf_size = 1;
@@ -513,7 +515,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->ch_offsets, &c->ch_range, &c->ch_scan_tmp, &c->ch_box, &c->ch_cent, &c->ch_slo, &c->ch_shi,
                      &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
-                     &c->ss_t, &c->ss_pix};
+                     &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
@@ -570,6 +572,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case BRE_OPT_SHARD_BLOCK:
         if (value < 1 || value > 4096) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_BLOCK must be in 1..4096");
         c->shard_block = (int)value;
+        return BRE_OK;
+    case BRE_OPT_SHARD_MODE:
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_MODE must be 0 or 1");
+        c->shard_mode = (int)value;
         return BRE_OK;
     case BRE_OPT_SHARD_COUNT:
         if (value < 1 || value > 65536) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_COUNT must be in 1..65536");
@@ -847,8 +853,8 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->cam_dev.as<DevCamera>(), c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
-                            c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count, c->shard_block,
-                            c->stream));
+                            c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count,
+                            c->shard_mode == 1 ? 0 : c->shard_block, c->stream));
     // total = offs[S-1] + valid[S-1]
     HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
     int64_t last_off = 0;
@@ -895,11 +901,41 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     const int64_t n = c->cam_nseg;
+    // packet sharding (BRE_OPT_SHARD_MODE 1): this rank gathers the 64-segment packets p = rank,
+    // rank + count, ... of the (sorted) order, copied into contiguous arrays first (bre_shard_segments)
+    const bool pshard = c->shard_mode == 1 && c->shard_count > 1;
     const bool sortable = c->kernel == 0 || c->kernel == 4;  // kernels 2 / 5 write in the caller's order
-    if (!c->sort_segments || n < 2 || (!sortable && (d_seg_rgb || d_seg_counts)))
+    const auto pick = [&](const float *o, const float *p, const float *d, const float *t, const int32_t *pix,
+                          const int32_t *index) -> bre_status {
+        const int64_t m = bre_shard_segments(n, c->shard_rank, c->shard_count);
+        if (m == 0) return BRE_OK;
+        const size_t M = (size_t)m;
+        HIPCHK(c, c->sp_o.ensure(M * 3 * sizeof(float)));
+        HIPCHK(c, c->sp_p.ensure(M * 3 * sizeof(float)));
+        HIPCHK(c, c->sp_d.ensure(M * 3 * sizeof(float)));
+        HIPCHK(c, c->sp_t.ensure(M * sizeof(float)));
+        HIPCHK(c, c->sp_pix.ensure(M * sizeof(int32_t)));
+        const bool want_index = d_seg_rgb || d_seg_counts;
+        if (want_index) HIPCHK(c, c->sp_index.ensure(M * sizeof(int32_t)));
+        HIPCHK(c, launch_packet_pick(n, m, c->shard_rank, c->shard_count, o, p, d, t, pix, index,
+                                     c->sp_o.as<float>(), c->sp_p.as<float>(), c->sp_d.as<float>(),
+                                     c->sp_t.as<float>(), c->sp_pix.as<int32_t>(),
+                                     want_index ? c->sp_index.as<int32_t>() : nullptr, c->stream));
+        return gather_device(c, m, c->sp_o.as<float>(), c->sp_p.as<float>(), c->sp_d.as<float>(),
+                             c->sp_t.as<float>(), c->sp_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
+                             d_seg_counts, want_index ? c->sp_index.as<int32_t>() : nullptr);
+    };
+    if (!c->sort_segments || n < 2 || (!sortable && (d_seg_rgb || d_seg_counts))) {
+        if (pshard) {
+            if (!sortable && (d_seg_rgb || d_seg_counts))
+                return fail(c, BRE_ERR_STATE, "packet shards with per-segment outputs need kernel 0 or 4");
+            return pick(c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(), c->seg_t.as<float>(),
+                        c->seg_pix.as<int32_t>(), nullptr);
+        }
         return gather_device(c, n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
                              c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
                              d_seg_counts);
+    }
     const size_t N = (size_t)n;
     HIPCHK(c, c->ss_bounds.ensure(8 * sizeof(unsigned int)));
     HIPCHK(c, c->ss_keys.ensure(N * sizeof(unsigned long long)));
@@ -920,6 +956,7 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
                c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
     // ss_vals_alt[i] = the camera-pass index of sorted segment i (the sort's permutation)
+    if (pshard) return pick(ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, c->ss_vals_alt.as<int32_t>());
     return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, d_seg_rgb, d_seg_counts,
                          (d_seg_rgb || d_seg_counts) ? c->ss_vals_alt.as<int32_t>() : nullptr);
 }
@@ -1207,6 +1244,17 @@ bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, 
     if (dseg) HIPCHK(c, hipMemcpyAsync(seg_rgb, dseg, S * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (dcnt) HIPCHK(c, hipMemcpyAsync(seg_counts, dcnt, S * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     return check_flags(c);
+}
+
+int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count) {
+    if (n_segments <= 0) return 0;
+    if (count <= 1) return n_segments;
+    if (rank < 0 || rank >= count) return 0;
+    const int64_t npk = (n_segments + 63) / 64;
+    const int64_t q = rank < npk ? (npk - 1 - rank) / count + 1 : 0;  // packets p = rank (mod count)
+    const int64_t last = npk - 1;                                      // the only partial packet
+    const int64_t tail = (last % count == rank) ? npk * 64 - n_segments : 0;
+    return q * 64 - tail;
 }
 
 float bre_beam_radius_at(float initial_radius, float alpha, int iteration) {

@@ -409,8 +409,11 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
     if (px >= C.width || py >= C.height) return;
     // image-tile sharding: this context walks only the reference's 16x16 camera-pass tiles
     // (photonbeam.cpp:345-347, 444-452) of the blocks of shard_block x shard_block tiles whose
-    // row-major block index = rank (mod count)
-    if (shard_count > 1) {
+    // row-major block index = rank (mod count).  shard_block 0 is the PACKET sharding: every tile is
+    // walked (the gather takes the rank's range of sorted packets) and the surface radiance of pixel p
+    // is added by rank p mod count only, so the ranks' films sum to the whole film.
+    const bool packet_shard = shard_block == 0;
+    if (shard_count > 1 && !packet_shard) {
         const int nbx = (((C.width + 15) >> 4) + shard_block - 1) / shard_block;
         if ((((py >> 4) / shard_block) * nbx + (px >> 4) / shard_block) % shard_count != shard_rank) return;
     }
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
             for (int c = 0; c < 3; ++c) beta[c] = beta[c] / cp;
         }
     }
-    if (surface && render_surfaces)
+    if (surface && render_surfaces && (!packet_shard || pixel % shard_count == shard_rank))
         for (int c = 0; c < 3; ++c) surface[3 * pixel + c] += Ld[c];
 }
 

@@ -212,6 +212,9 @@ struct SegSort {
 };
 size_t seg_sort_temp_bytes(int64_t n);
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);
+hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, const float *o, const float *p,
+                              const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
+                              float *p2, float *d2, float *t2, int32_t *pix2, int32_t *index2, hipStream_t st);
 
 // gather kernels (bre_gather.hip)
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);

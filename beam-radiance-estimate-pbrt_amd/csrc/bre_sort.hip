@@ -181,7 +181,41 @@ __global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// Packet shards: copy this shard's packets (64-segment packets p = rank, rank + count, ... of the
+// sorted order) into contiguous arrays; out_index (optional) carries the source's caller index.
+__global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, int rank, int count,
+                                                        const float *__restrict__ o, const float *__restrict__ p,
+                                                        const float *__restrict__ d, const float *__restrict__ t,
+                                                        const int32_t *__restrict__ pix,
+                                                        const int32_t *__restrict__ index, float *__restrict__ o2,
+                                                        float *__restrict__ p2, float *__restrict__ d2,
+                                                        float *__restrict__ t2, int32_t *__restrict__ pix2,
+                                                        int32_t *__restrict__ index2) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= m) return;
+    const int64_t src = ((j >> 6) * count + rank) * 64 + (j & 63);  // < n for j < m (shard_segments)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        o2[3 * j + k] = o[3 * src + k];
+        p2[3 * j + k] = p[3 * src + k];
+        d2[3 * j + k] = d[3 * src + k];
+    }
+    t2[j] = t[src];
+    pix2[j] = pix[src];
+    if (index2) index2[j] = index ? index[src] : (int32_t)src;
+    (void)n;
+}
+
 }  // namespace
+
+hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, const float *o, const float *p,
+                              const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
+                              float *p2, float *d2, float *t2, int32_t *pix2, int32_t *index2, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_packet_pick, dim3(grid_of(m)), dim3(kBlock), 0, st, n, m, rank, count, o, p, d, t, pix, index,
+                       o2, p2, d2, t2, pix2, index2);
+    return hipGetLastError();
+}
 
 size_t seg_sort_temp_bytes(int64_t n) {
     size_t bytes = 0;

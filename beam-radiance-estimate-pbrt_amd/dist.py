@@ -1,4 +1,4 @@
-"""Multi-GPU decomposition of the gather: image tiles across ranks, beams replicated.
+"""Multi-GPU decomposition of the gather: image tiles (or packet ranges) across ranks, beams replicated.
 
 The reference's camera pass already works in 16x16 pixel tiles (photonbeam.cpp:345-347, 444-557);
 here those tiles are dealt round-robin to the ranks (one process per GPU; libbre's camera pass walks
@@ -10,6 +10,13 @@ every rank packs the pixels of its own tiles into a contiguous band (1/N of the 
 are gathered to the root over RCCL (backend "nccl") or gloo (CPU tests), which scatters them back
 into the full film.  Ownership is disjoint, so the gathered film equals the sum of the ranks'
 partial films exactly.
+
+Packet shards (``packets=True``, BRE_OPT_SHARD_MODE 1, the bench's default for strong scaling): every
+rank runs the whole camera pass and sorts all segments as one GPU would, then gathers only its
+round-robin share of the sorted 64-segment packets (p = rank mod N, ``bre_shard_segments``), so its
+packets are exactly the single-GPU packets and every rank gets the same mix of cheap and costly ones (tile shards thin out each rank's bounce segments N-fold and loosen its
+packets: 1.5M vs 2.3M estimates/s per GPU at N=8, profiles/r2/explore/explore28-29).  A pixel's
+segments may then sit on several ranks: the films are partial sums, combined by one RCCL reduce.
 """
 from __future__ import annotations
 
@@ -37,15 +44,19 @@ def tile_pixels(w: int, h: int, rank: int, world: int, tile: int = 16, block: in
 class ShardedFrame:
     """Full-resolution RGB accumulation buffer of one rank (only its own tiles are ever written)."""
 
-    def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16, block: int = 1):
+    def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16, block: int = 1,
+                 packets: bool = False):
         import torch
 
         self.w, self.h, self.rank, self.world, self.tile, self.block = w, h, rank, world, tile, block
-        self.pixels = tile_pixels(w, h, rank, world, tile, block)
+        # packets=True: PACKET shards (BRE_OPT_SHARD_MODE 1) -- every rank may write every pixel (its
+        # range of the sorted segment packets), and the films are SUMMED by one reduce
+        self.packets = packets
+        self.pixels = np.arange(w * h, dtype=np.int64) if packets else tile_pixels(w, h, rank, world, tile, block)
         self.accum = torch.zeros((w * h, 3), dtype=torch.float32, device=device)
         self.device = device
         self._band = None
-        if world > 1:
+        if world > 1 and not packets:
             counts = [tile_pixels(w, h, r, world, tile, block).shape[0] for r in range(world)]
             self.band_len = max(counts)
             self._idx = torch.from_numpy(self.pixels).to(device)
@@ -79,6 +90,9 @@ class ShardedFrame:
         import torch.distributed as dist
 
         if self.world == 1:
+            return self.accum
+        if self.packets:  # partial films of one image: one sum-reduce to the root
+            dist.reduce(self.accum, dst=root, op=dist.ReduceOp.SUM)
             return self.accum
         band = self.band()
         parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None

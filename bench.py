@@ -14,10 +14,14 @@ schedule and sampler indices included), so `--steps 16` is exactly the C2 render
 Multi-GPU (`--gpus N`): one process per GPU.  Launched by torch.distributed.run (WORLD_SIZE set) it
 joins that group; launched alone with N > 1 it starts N rank processes itself (a torch.distributed.run
 child, before any GPU call) and exits with its status.  Default scaling is STRONG: one film (the
-workload's W x H) whose 16x16 tiles (photonbeam.cpp:345-347) are dealt round-robin to the ranks; every
-rank traces the same photons (per-photon PCG32 sequences, no communication) and builds its own BVH;
-the ranks' bands of owned pixels are gathered to rank 0 once per written image (the last step), one
-RCCL gather.  `--scaling weak` gives every rank its own film of the same size (N independent renders).
+workload's W x H); every rank traces the same photons (per-photon PCG32 sequences, no communication),
+builds its own BVH, runs the whole camera pass and sorts all segments, then gathers its round-robin
+share of the sorted 64-segment packets (`--shard-mode packets`, libbre BRE_OPT_SHARD_MODE 1: exactly the
+single-GPU packets, every rank the same mix); the partial films are summed to rank 0 once per written image
+(the last step), one RCCL reduce.  `--shard-mode tiles` deals the reference's 16x16 tiles
+(photonbeam.cpp:345-347) instead, in blocks of `--shard-block`^2, with one RCCL gather of the owned
+pixel bands.  `--scaling weak` gives every rank its own film of the same size (N independent renders).
+`--emulate-shard R/N` runs rank R's share of an N-GPU strong-scaling run alone on one GPU.
 
 Also reported (rank 0, N = 1):
 * `roofline` — HBM: the tile kernel's algorithmic bytes per launch (what its packets must read: node
@@ -82,8 +86,11 @@ def parse(argv=None):
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--shard-mode", choices=["packets", "tiles"], default="packets",
+                    help="strong scaling: each GPU gathers a range of the sorted segment packets (default) "
+                         "or owns image tiles")
     ap.add_argument("--shard-block", type=int, default=1,
-                    help="strong scaling: tiles per side of the image blocks dealt round-robin to the GPUs")
+                    help="tile shards: tiles per side of the image blocks dealt round-robin to the GPUs")
     ap.add_argument("--emulate-shard", type=str, default=None, help=argparse.SUPPRESS)  # "R/N": rank R's share on 1 GPU
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -167,7 +174,8 @@ def main():
     srank, scount = (rank, world) if strong else (0, 1)
     if args.emulate_shard and world == 1:  # one rank's share of an N-GPU strong-scaling run, on this GPU
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
-    frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block)
+    frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
+                              packets=args.shard_mode == "packets")
     g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
                        prefilter=bool(args.prefilter))
     g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
@@ -428,7 +436,8 @@ class SceneWorkload:
         else:
             self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
-        g.set_shard(shard_rank, shard_count, frame.block)
+        g.set_shard(shard_rank, shard_count, frame.block, frame.packets)
+        self.shard = (shard_rank, shard_count)
         self.ld = frame.accum
         self.scratch = torch.zeros_like(self.ld)
         self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "
@@ -450,6 +459,8 @@ class SceneWorkload:
         g.gather_camera(R, ld)
         if ev is not None:
             ev[1].record()
+        if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
+            n = self.bre.shard_segments(n, *self.shard)
         self.last_nseg = n
         return n
 
@@ -480,13 +491,17 @@ class SceneWorkload:
         a = self.args
         med = ("homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)" if WORKLOADS[self.name]["medium"] == "fog" else
                f"GridDensityMedium smoke {a.grid_n}^3 (sigma_a 0.5, sigma_s 4.5, g 0.7)")
-        film = (f"{a.width}x{a.height} split by 16x16 tiles over the GPUs" if a.scaling == "strong" else
-                f"{a.width}x{a.height} per GPU")
+        film = (f"{a.width}x{a.height} per GPU" if a.scaling != "strong" else
+                f"{a.width}x{a.height}, the sorted segment packets split over the GPUs" if a.shard_mode == "packets"
+                else f"{a.width}x{a.height} split by 16x16 tiles over the GPUs")
         return {"workload": f"{self.name.upper()}: Cornell box + {med}, {a.photons / 1e6:g}M photons/iteration, "
                             f"{film}, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
                 "photons_per_iteration": a.photons, "image": [self.W, self.H], "iterations_timed": a.steps,
-                "parallelism": f"image tiles x{world} ({a.scaling} scaling), photons traced on every rank, "
-                               "one RCCL gather of the owned-pixel bands per written image",
+                "parallelism": (f"segment packets x{world} ({a.scaling} scaling), photons traced and camera pass "
+                                "on every rank, one RCCL reduce of the partial films per written image"
+                                if a.shard_mode == "packets" else
+                                f"image tiles x{world} ({a.scaling} scaling), photons traced on every rank, "
+                                "one RCCL gather of the owned-pixel bands per written image"),
                 "kernel": KERNEL_NAMES.get(a.kernel, str(a.kernel)), "split": a.split,
                 "prefilter": bool(a.prefilter), "sort_segments": bool(a.sort_segments)}
 
