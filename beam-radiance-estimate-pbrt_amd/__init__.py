@@ -109,7 +109,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = I32
     lib.bre_beam_radius_at.argtypes = [F, F, I32]
     lib.bre_beam_radius_at.restype = F
-    lib.bre_shard_segments.argtypes = [I64, I32, I32]
+    lib.bre_shard_segments.argtypes = [I64, I32, I32, I32]
     lib.bre_shard_segments.restype = I64
     lib.bre_resolve_image.argtypes = [I64, P, I32, P]
     lib.bre_resolve_image.restype = I32
@@ -189,8 +189,9 @@ class BeamGather:
     def set_shard(self, rank: int, count: int, block: int = 1, packets: bool = False):
         """Tile shards (default): the camera pass walks only the 16x16 image tiles of the blocks of
         block x block tiles whose row-major block index is rank (mod count) (dist.tile_pixels lists the
-        same pixels).  packets=True: the whole camera pass, and the gather of this rank's range of the
-        sorted packets (shard_range); the ranks' films sum to the whole film."""
+        same pixels).  packets=True: the whole camera pass, and the gather of this rank's chunks of
+        `block` consecutive sorted packets, chunk c to rank c mod count (shard_packet_index); the ranks'
+        films sum to the whole film."""
         self.set_option(OPT_SHARD_MODE, 1 if packets else 0)
         self.set_option(OPT_SHARD_BLOCK, int(block))
         self.set_option(OPT_SHARD_COUNT, int(count))
@@ -330,17 +331,21 @@ class BeamGather:
         self.close()
 
 
-def shard_segments(n_segments: int, rank: int, count: int) -> int:
+def shard_segments(n_segments: int, rank: int, count: int, chunk: int = 1) -> int:
     """How many camera segments shard `rank` of `count` gathers in packet mode (libbre)."""
-    return int(load_library().bre_shard_segments(int(n_segments), int(rank), int(count)))
+    return int(load_library().bre_shard_segments(int(n_segments), int(rank), int(count), int(chunk)))
 
 
-def shard_packet_index(n_segments: int, rank: int, count: int):
-    """The segment indices (in the gathered order) of shard `rank`'s packets p = rank (mod count): the
-    host view of libbre's packet pick, for tests and CPU rehearsals."""
+def shard_packet_index(n_segments: int, rank: int, count: int, chunk: int = 1):
+    """The segment indices (in the gathered order) of shard `rank`'s packets -- chunks of `chunk`
+    consecutive packets, chunk c to shard c mod count: the host view of libbre's packet pick, for tests
+    and CPU rehearsals."""
     import numpy as np
     npk = (int(n_segments) + 63) // 64
-    idx = (np.arange(rank, npk, count, dtype=np.int64)[:, None] * 64 + np.arange(64)[None, :]).ravel()
+    nch = (npk + chunk - 1) // chunk
+    pk = (np.arange(rank, nch, count, dtype=np.int64)[:, None] * chunk + np.arange(chunk)[None, :]).ravel()
+    pk = pk[pk < npk]
+    idx = (pk[:, None] * 64 + np.arange(64)[None, :]).ravel()
     return idx[idx < n_segments]
 
 

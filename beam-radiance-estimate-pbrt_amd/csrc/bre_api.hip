@@ -60,7 +60,7 @@ struct bre_ctx {
     int split = 256;         // work roots per packet (r2: 64 with the rotated block map, C2 +42% over 8; 256 +2% on the final kernel, partials 3 KB per segment)
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
-    int block_map = 1;       // internal: tile kernel block mapping (GatherArgs::block_map): 1 rotated
+    int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
     int occupancy = 7;       // tile kernel register budget (min waves per SIMD): 7 measured best (r2, no-SLP build: 71 VGPRs)
     int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
@@ -593,7 +593,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
     case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated (sweeps)
-        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0..3");
         c->block_map = (int)value;
         return BRE_OK;
     case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)
@@ -901,13 +901,14 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     const int64_t n = c->cam_nseg;
-    // packet sharding (BRE_OPT_SHARD_MODE 1): this rank gathers the 64-segment packets p = rank,
-    // rank + count, ... of the (sorted) order, copied into contiguous arrays first (bre_shard_segments)
+    // packet sharding (BRE_OPT_SHARD_MODE 1): this rank gathers the chunks c = rank (mod count) of
+    // BRE_OPT_SHARD_BLOCK consecutive 64-segment packets of the (sorted) order, copied into contiguous
+    // arrays first (bre_shard_segments)
     const bool pshard = c->shard_mode == 1 && c->shard_count > 1;
     const bool sortable = c->kernel == 0 || c->kernel == 4;  // kernels 2 / 5 write in the caller's order
     const auto pick = [&](const float *o, const float *p, const float *d, const float *t, const int32_t *pix,
                           const int32_t *index) -> bre_status {
-        const int64_t m = bre_shard_segments(n, c->shard_rank, c->shard_count);
+        const int64_t m = bre_shard_segments(n, c->shard_rank, c->shard_count, c->shard_block);
         if (m == 0) return BRE_OK;
         const size_t M = (size_t)m;
         HIPCHK(c, c->sp_o.ensure(M * 3 * sizeof(float)));
@@ -917,7 +918,7 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
         HIPCHK(c, c->sp_pix.ensure(M * sizeof(int32_t)));
         const bool want_index = d_seg_rgb || d_seg_counts;
         if (want_index) HIPCHK(c, c->sp_index.ensure(M * sizeof(int32_t)));
-        HIPCHK(c, launch_packet_pick(n, m, c->shard_rank, c->shard_count, o, p, d, t, pix, index,
+        HIPCHK(c, launch_packet_pick(n, m, c->shard_rank, c->shard_count, c->shard_block, o, p, d, t, pix, index,
                                      c->sp_o.as<float>(), c->sp_p.as<float>(), c->sp_d.as<float>(),
                                      c->sp_t.as<float>(), c->sp_pix.as<int32_t>(),
                                      want_index ? c->sp_index.as<int32_t>() : nullptr, c->stream));
@@ -1246,15 +1247,16 @@ bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, 
     return check_flags(c);
 }
 
-int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count) {
+int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int32_t chunk) {
     if (n_segments <= 0) return 0;
     if (count <= 1) return n_segments;
-    if (rank < 0 || rank >= count) return 0;
-    const int64_t npk = (n_segments + 63) / 64;
-    const int64_t q = rank < npk ? (npk - 1 - rank) / count + 1 : 0;  // packets p = rank (mod count)
-    const int64_t last = npk - 1;                                      // the only partial packet
-    const int64_t tail = (last % count == rank) ? npk * 64 - n_segments : 0;
-    return q * 64 - tail;
+    if (rank < 0 || rank >= count || chunk < 1) return 0;
+    const int64_t npk = (n_segments + 63) / 64, K = chunk;
+    const int64_t nch = (npk + K - 1) / K;                              // chunks of K packets
+    const int64_t q = rank < nch ? (nch - 1 - rank) / count + 1 : 0;    // chunks c = rank (mod count)
+    const bool last = (nch - 1) % count == rank;                        // owns the only partial chunk
+    const int64_t packets = q * K - (last ? nch * K - npk : 0);
+    return packets * 64 - (last ? npk * 64 - n_segments : 0);
 }
 
 float bre_beam_radius_at(float initial_radius, float alpha, int iteration) {

@@ -212,7 +212,7 @@ struct SegSort {
 };
 size_t seg_sort_temp_bytes(int64_t n);
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);
-hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, const float *o, const float *p,
+hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,
                               const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
                               float *p2, float *d2, float *t2, int32_t *pix2, int32_t *index2, hipStream_t st);
 

@@ -513,7 +513,12 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     // L2 serves one eighth of the tree).  Speed only, never correctness.
     int sub;
     int64_t grp;
-    if (map == 1) {
+    if (map == 3) {
+        // LPT: all packets on the largest subtree (roots are sorted by size), then the next, ...
+        const unsigned P = gridDim.x / (unsigned)S;
+        grp = blockIdx.x % P;
+        sub = (int)(blockIdx.x / P);
+    } else if (map == 1) {
         grp = blockIdx.x / (unsigned)S;
         sub = (int)((blockIdx.x % (unsigned)S + grp) % (unsigned)S);
     } else if (map == 2 || S < 8) {
@@ -931,19 +936,23 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
     }
 }
 
-// Work roots: the BVH frontier at depth log2(S) (leaves above it stay in the frontier).
-__global__ void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    int32_t cur[kMaxSplit], nxt[kMaxSplit];
-    int n = 1;
-    cur[0] = 0;
-    while (true) {
-        int m = 0;
-        bool fits = true;
-        for (int i = 0; i < n; ++i) m += (cur[i] >= 0) ? 2 : 1;
-        if (m > S) fits = false;
-        bool grew = false;
-        if (fits) {
+// Work roots: the BVH frontier at depth log2(S) (leaves above it stay in the frontier), ordered by the
+// number of leaf tiles below each root, largest first (stable): with block map 3 every packet's
+// waves on the largest subtrees are dispatched first and the kernel's tail is made of small ones.
+// The leaves below a Karras node are a contiguous range (bre_build.hip), found by its leftmost and
+// rightmost descents.  The partial sums are added in this root order (k_reduce): deterministic.
+__global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
+    __shared__ int32_t cur[kMaxSplit], nxt[kMaxSplit], wt[kMaxSplit];
+    __shared__ int n_sh;
+    if (blockIdx.x != 0) return;
+    if (threadIdx.x == 0) {
+        int n = 1;
+        cur[0] = 0;
+        while (true) {
+            int m = 0;
+            for (int i = 0; i < n; ++i) m += (cur[i] >= 0) ? 2 : 1;
+            if (m > S) break;
+            bool grew = false;
             m = 0;
             for (int i = 0; i < n; ++i) {
                 if (cur[i] >= 0) {
@@ -955,14 +964,43 @@ __global__ void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restri
                     nxt[m++] = cur[i];
                 }
             }
+            if (!grew) break;
+            for (int i = 0; i < m; ++i) cur[i] = nxt[i];
+            n = m;
         }
-        if (!fits || !grew) break;
-        for (int i = 0; i < m; ++i) cur[i] = nxt[i];
-        n = m;
+        n_sh = n;
     }
-    for (int i = 0; i < n; ++i) roots[i] = cur[i];
-    for (int i = n; i < S; ++i) roots[i] = kEmptyChild;
-    roots[S] = n;
+    __syncthreads();
+    const int n = n_sh;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int32_t lo = cur[i], hi = cur[i];
+        while (lo >= 0) {
+            const Node &nd = nodes[lo];
+            lo = nd.child[0] != kEmptyChild ? nd.child[0] : nd.child[1];
+        }
+        while (hi >= 0) {
+            const Node &nd = nodes[hi];
+            hi = nd.child[1] != kEmptyChild ? nd.child[1] : nd.child[0];
+        }
+        wt[i] = (~hi) - (~lo) + 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < n; ++i) {  // stable insertion sort, weight descending
+            const int32_t r = cur[i], w = wt[i];
+            int j = i - 1;
+            while (j >= 0 && wt[j] < w) {
+                cur[j + 1] = cur[j];
+                wt[j + 1] = wt[j];
+                --j;
+            }
+            cur[j + 1] = r;
+            wt[j + 1] = w;
+        }
+        for (int i = 0; i < n; ++i) roots[i] = cur[i];
+        for (int i = n; i < S; ++i) roots[i] = kEmptyChild;
+        roots[S] = n;
+    }
 }
 
 template <bool COUNT>
@@ -1045,7 +1083,7 @@ __global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *_
 }  // namespace
 
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s) {
-    hipLaunchKernelGGL(k_roots, dim3(1), dim3(64), 0, s, nodes, S, roots);
+    hipLaunchKernelGGL(k_roots, dim3(1), dim3(256), 0, s, nodes, S, roots);
     return hipGetLastError();
 }
 

@@ -181,9 +181,10 @@ __global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Packet shards: copy this shard's packets (64-segment packets p = rank, rank + count, ... of the
-// sorted order) into contiguous arrays; out_index (optional) carries the source's caller index.
-__global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, int rank, int count,
+// Packet shards: copy this shard's packets into contiguous arrays -- the sorted order's 64-segment
+// packets in chunks of `chunk` consecutive packets, chunk c to shard c mod count (bre_shard_segments);
+// index2 (optional) carries the source's caller index.
+__global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk,
                                                         const float *__restrict__ o, const float *__restrict__ p,
                                                         const float *__restrict__ d, const float *__restrict__ t,
                                                         const int32_t *__restrict__ pix,
@@ -193,7 +194,8 @@ __global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, in
                                                         int32_t *__restrict__ index2) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= m) return;
-    const int64_t src = ((j >> 6) * count + rank) * 64 + (j & 63);  // < n for j < m (shard_segments)
+    const int64_t g = j >> 6;  // this shard's packet ordinal: chunk g / chunk, packet g % chunk in it
+    const int64_t src = (((g / chunk) * count + rank) * chunk + g % chunk) * 64 + (j & 63);  // < n for j < m
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         o2[3 * j + k] = o[3 * src + k];
@@ -208,11 +210,11 @@ __global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, in
 
 }  // namespace
 
-hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, const float *o, const float *p,
+hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,
                               const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
                               float *p2, float *d2, float *t2, int32_t *pix2, int32_t *index2, hipStream_t st) {
     if (m <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_packet_pick, dim3(grid_of(m)), dim3(kBlock), 0, st, n, m, rank, count, o, p, d, t, pix, index,
+    hipLaunchKernelGGL(k_packet_pick, dim3(grid_of(m)), dim3(kBlock), 0, st, n, m, rank, count, chunk, o, p, d, t, pix, index,
                        o2, p2, d2, t2, pix2, index2);
     return hipGetLastError();
 }

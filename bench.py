@@ -460,7 +460,7 @@ class SceneWorkload:
         if ev is not None:
             ev[1].record()
         if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
-            n = self.bre.shard_segments(n, *self.shard)
+            n = self.bre.shard_segments(n, *self.shard, self.frame.block)
         self.last_nseg = n
         return n
 

@@ -90,9 +90,9 @@ typedef enum bre_option {
     BRE_OPT_SORT_SEGMENTS = 13, /* bre_gather_camera: 0/1 hand the camera-pass segments to the gather
                                   in 6-D Morton order of (origin, end point) (default 1); pixel sums
                                   are the same pair contributions either way */
-    BRE_OPT_SHARD_BLOCK = 14, /* camera pass: tiles per side of the blocks dealt to the shards (1..4096,
-                                default 1); larger blocks keep a shard's bounce segments as dense in
-                                space as the whole film's, so its packets stay coherent */
+    BRE_OPT_SHARD_BLOCK = 14, /* tile shards: tiles per side of the blocks dealt to the shards; packet
+                                shards: consecutive packets per chunk dealt to the shards (1..4096,
+                                default 1) */
     BRE_OPT_SHARD_MODE = 15  /* 0 (default): shards own image tiles (SHARD_BLOCK), each pixel is written
                                 by one shard.  1: PACKET shards -- every shard runs the whole camera
                                 pass and gathers its round-robin share of the sorted 64-segment packets
@@ -239,9 +239,10 @@ bre_status bre_render_progressive(bre_ctx *ctx, const bre_scene *scene, const br
 /* R_i for iteration i: R_{k+1} = R_k * (k + alpha) / (k + 1), R_0 = initial, in float. */
 float bre_beam_radius_at(float initial_radius, float alpha, int iteration);
 /* How many of n_segments camera segments shard `rank` of `count` gathers under BRE_OPT_SHARD_MODE 1:
-   the 64-segment packets p = rank, rank + count, rank + 2 count, ... of the (sorted) order (dealt
-   round-robin, so every shard gets the same mix of cheap primary and costly bounce packets). */
-int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count);
+   the (sorted) order's 64-segment packets form chunks of `chunk` consecutive packets (the context's
+   BRE_OPT_SHARD_BLOCK), dealt round-robin -- chunk c to shard c % count -- so every shard gets the same
+   mix of cheap primary and costly bounce packets while its concurrent packets stay neighbours. */
+int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int32_t chunk);
 /* image = Ld / (iter + 1) for npix pixels (host arrays). */
 bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, float *out_rgb);
 

@@ -57,10 +57,10 @@ def test_sharded_render_equals_single_shard(bre, scene_mod_gpu, world, shape, ph
     assert (np.abs(got - want)[big] <= 1e-4 * np.abs(want[big]).max(axis=1, keepdims=True)).all()
 
 
-@pytest.mark.parametrize("world", [3, 8])
-def test_packet_shards_sum_to_single_render(bre, scene_mod_gpu, world):
+@pytest.mark.parametrize("world,chunk", [(3, 1), (8, 1), (8, 4)])
+def test_packet_shards_sum_to_single_render(bre, scene_mod_gpu, world, chunk):
     """Packet shards (BRE_OPT_SHARD_MODE 1): every shard runs the whole camera pass and gathers its
-    round-robin share of the sorted packets; the shares partition the segments and the partial films
+    round-robin share of the sorted packets (chunks of `chunk`); the shares partition the segments and the partial films
     sum to the single-GPU film (what the RCCL reduce of dist.ShardedFrame(packets=True) computes)."""
     dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
     W, H = 256, 192
@@ -69,7 +69,7 @@ def test_packet_shards_sum_to_single_render(bre, scene_mod_gpu, world):
 
     def render(rank, count, frame):
         with bre.BeamGather(0) as g:
-            g.set_shard(rank, count, packets=True)
+            g.set_shard(rank, count, chunk, packets=True)
             g.trace_photons(scene, 200_000, it, 5, R)
             n = g.camera_pass(scene, W, H, it, 5, True, True, surface=frame.accum)
             g.gather_camera(R, frame.accum)
@@ -78,12 +78,12 @@ def test_packet_shards_sum_to_single_render(bre, scene_mod_gpu, world):
 
     ref = dmod.ShardedFrame(W, H, 0, 1, device="cuda")
     n_ref = render(0, 1, ref)
-    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda", packets=True) for r in range(world)]
+    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda", block=chunk, packets=True) for r in range(world)]
     ns = [render(r, world, f) for r, f in enumerate(frames)]
     assert all(n == n_ref for n in ns)  # every shard runs the whole camera pass
-    assert sum(bre.shard_segments(n_ref, r, world) for r in range(world)) == n_ref
-    assert np.array_equal(np.sort(np.concatenate([bre.shard_packet_index(n_ref, r, world) for r in range(world)])),
-                          np.arange(n_ref))
+    assert sum(bre.shard_segments(n_ref, r, world, chunk) for r in range(world)) == n_ref
+    parts = [bre.shard_packet_index(n_ref, r, world, chunk) for r in range(world)]
+    assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(n_ref))
     got = sum(f.accum.double() for f in frames).float().cpu().numpy()
     want = ref.accum.cpu().numpy()
     assert _rel_l2(got, want) <= 1e-6
