@@ -86,6 +86,9 @@ def parse(argv=None):
     ap.add_argument("--sort-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
+                         "camera pass overlapping iteration k's gather (0: one context)")
     ap.add_argument("--shard-mode", choices=["packets", "tiles"], default="packets",
                     help="strong scaling: each GPU gathers a range of the sorted segment packets (default) "
                          "or owns image tiles")
@@ -176,30 +179,37 @@ def main():
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
                               packets=args.shard_mode == "packets")
-    g = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
-                       prefilter=bool(args.prefilter))
-    g.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
-    if args.kernel == 5:
-        g.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
-        g.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
-    if args.occupancy:
-        g.set_option(102, args.occupancy)
-    if args.tile_leaf:
-        g.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
-    if args.block_map >= 0:
-        g.set_option(107, args.block_map)
-    if args.sort_key >= 0:
-        g.set_option(105, args.sort_key)
-    if args.tscan >= 0:
-        g.set_option(108, args.tscan)
-    # one explicit stream shared by libbre and torch: the HIP events that time the gather kernel
-    # are recorded on the stream the kernel runs on
-    stream = torch.cuda.Stream(dev)
+    def make_ctx():
+        c = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
+                           prefilter=bool(args.prefilter))
+        c.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
+        if args.kernel == 5:
+            c.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
+            c.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
+        if args.occupancy:
+            c.set_option(102, args.occupancy)
+        if args.tile_leaf:
+            c.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
+        if args.block_map >= 0:
+            c.set_option(107, args.block_map)
+        if args.sort_key >= 0:
+            c.set_option(105, args.sort_key)
+        if args.tscan >= 0:
+            c.set_option(108, args.tscan)
+        # one explicit stream per context, shared with torch: the HIP events that time the gather
+        # kernel are recorded on the stream the kernel runs on
+        st = torch.cuda.Stream(dev)
+        c.set_stream(st.cuda_stream)
+        return c, st
+
+    g, stream = make_ctx()
     torch.cuda.set_stream(stream)
-    g.set_stream(stream.cuda_stream)
 
     if args.workload != "synthetic":
-        wl = SceneWorkload(args, bre, g, frame, srank, scount)
+        # --pipeline 1: a second context on a second stream, iterations alternating between them, so
+        # iteration k+1's photon pass, BVH build and camera pass overlap iteration k's gather
+        extra = [make_ctx()] if (args.pipeline and not args.pmc_child) else []
+        wl = SceneWorkload(args, bre, [(g, stream)] + extra, frame, srank, scount)
     else:
         wl = SyntheticWorkload(args, bre, g, frame, dev)
 
@@ -225,8 +235,10 @@ def main():
             torch.cuda.synchronize(dev)
             print(f"bench.py: rank {rank} step {k + 1}/{args.steps} done at {time.perf_counter() - t0:.1f} s",
                   file=sys.stderr, flush=True)
-        if k == args.steps - 1 and strong and world > 1:
-            frame.gather_to_root(0)  # one RCCL gather per written image
+        if k == args.steps - 1:
+            wl.finish()  # the pipeline's second film into the frame
+            if strong and world > 1:
+                frame.gather_to_root(0)  # one RCCL reduce / gather per written image
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -300,6 +312,7 @@ def main():
         # the counter pass and the PMC passes run iteration 0: hold its bytes to timed iteration 0's
         # HIP-event launch time (the average over the timed launches is gather_kernel_ms)
         result["roofline"] = roofline(st, args, wl, gather_per_step[0], pmc, cpu)
+    wl.close()
     g.close()
     if rank == 0:
         line = json.dumps(result)
@@ -424,10 +437,12 @@ class SceneWorkload:
     sigma_s 0.5, g 0); c3/c5 the same box filled with a 64^3 GridDensityMedium of seeded value-noise
     smoke (sigma_a 0.5, sigma_s 4.5, g 0.7); c4 the fog at 2048^2 with 20M photons."""
 
-    def __init__(self, args, bre, g, frame, shard_rank, shard_count):
+    def __init__(self, args, bre, ctxs, frame, shard_rank, shard_count):
         import torch
 
         sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
+        self.ctxs = ctxs  # [(BeamGather, torch stream)]: 1, or 2 when pipelined
+        g = ctxs[0][0]
         self.args, self.bre, self.g, self.frame = args, bre, g, frame
         self.name = args.workload
         preset = WORKLOADS[args.workload]
@@ -436,10 +451,14 @@ class SceneWorkload:
         else:
             self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
-        g.set_shard(shard_rank, shard_count, frame.block, frame.packets)
+        for c, _ in ctxs:
+            c.set_shard(shard_rank, shard_count, frame.block, frame.packets)
         self.shard = (shard_rank, shard_count)
         self.ld = frame.accum
-        self.scratch = torch.zeros_like(self.ld)
+        # one film per context: the camera pass adds surface radiance without atomics, so two
+        # iterations in flight must not share a buffer; finish() sums them
+        self.films = [self.ld] + [torch.zeros_like(self.ld) for _ in ctxs[1:]]
+        self.scratch = [torch.zeros_like(self.ld) for _ in ctxs]
         self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "
                      f"{'grid-density smoke' if preset['medium'] == 'smoke' else 'homogeneous fog'}; photons and "
                      "camera paths traced on the GPU)")
@@ -449,20 +468,41 @@ class SceneWorkload:
         return self.bre.beam_radius_at(self.args.radius, self.args.alpha, it)
 
     def step(self, it, ev, scratch):
-        a, g = self.args, self.g
-        ld = self.scratch if scratch else self.ld
+        import torch
+
+        a = self.args
+        i = it % len(self.ctxs)
+        g, st = self.ctxs[i]
+        ld = (self.scratch if scratch else self.films)[i]
         R = self.radius(it)
-        self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
-        n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
-        if ev is not None:
-            ev[0].record()
-        g.gather_camera(R, ld)
-        if ev is not None:
-            ev[1].record()
+        with torch.cuda.stream(st):
+            self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
+            n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
+            if ev is not None:
+                ev[0].record()
+            g.gather_camera(R, ld)  # asynchronous: the next step's passes overlap it on the other stream
+            if ev is not None:
+                ev[1].record()
         if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
             n = self.bre.shard_segments(n, *self.shard, self.frame.block)
         self.last_nseg = n
         return n
+
+    def finish(self):
+        """Sum the pipeline's films into the frame (on the first context's stream, after both)."""
+        import torch
+
+        if len(self.films) > 1:
+            st0 = self.ctxs[0][1]
+            for _, st in self.ctxs[1:]:
+                st0.wait_stream(st)
+            with torch.cuda.stream(st0):
+                for f in self.films[1:]:
+                    self.films[0].add_(f)
+
+    def close(self):
+        for c, _ in self.ctxs[1:]:
+            c.close()
 
     def diagnostics(self):
         import torch
@@ -549,6 +589,12 @@ class SyntheticWorkload:
 
     def segments_per_gather(self):
         return self.nseg
+
+    def finish(self):
+        pass
+
+    def close(self):
+        pass
 
     def cpu_inputs(self, it):
         return self.beams, self.segs, self.args.radius
