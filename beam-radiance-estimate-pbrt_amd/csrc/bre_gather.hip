@@ -50,9 +50,10 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #define BRE_RMW_MAX_RUNS 8
 #endif
 // BRE_NODE_RELOAD 1: the production instantiation re-reads o, tmax, 1/d from the SegRec at each node
-// visit (register budget); 0 keeps them in registers
+// visit (register budget, occupancy 7); 0 (default) keeps them in registers at occupancy 6, +1.5% at
+// C2 and C3 once the LPT order made the node loads cheap (explore38)
 #ifndef BRE_NODE_RELOAD
-#define BRE_NODE_RELOAD 1
+#define BRE_NODE_RELOAD 0
 #endif
 // BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
 // BRE_NODE_PREFETCH 1: the traversal requests the next node's record before scanning the pending leaves
