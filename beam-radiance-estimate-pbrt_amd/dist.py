@@ -92,7 +92,13 @@ class ShardedFrame:
         if self.world == 1:
             return self.accum
         if self.packets:  # partial films of one image: one sum-reduce to the root
-            dist.reduce(self.accum, dst=root, op=dist.ReduceOp.SUM)
+            if dist.get_backend() == "gloo" and self.accum.is_cuda:  # gloo reduces host tensors
+                host = self.accum.cpu()
+                dist.reduce(host, dst=root, op=dist.ReduceOp.SUM)
+                if self.rank == root:
+                    self.accum.copy_(host)
+            else:
+                dist.reduce(self.accum, dst=root, op=dist.ReduceOp.SUM)
             return self.accum
         band = self.band()
         parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None

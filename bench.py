@@ -95,6 +95,9 @@ def parse(argv=None):
     ap.add_argument("--shard-block", type=int, default=1,
                     help="tile shards: tiles per side of the image blocks dealt round-robin to the GPUs")
     ap.add_argument("--emulate-shard", type=str, default=None, help=argparse.SUPPRESS)  # "R/N": rank R's share on 1 GPU
+    # rehearsal of the N-rank flow on a one-GPU box: every rank on cuda:0, collectives over gloo
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
+    ap.add_argument("--share-gpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline gather time (all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed counters/timing pass (profiling runs)")
@@ -162,8 +165,13 @@ def main():
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if env_world > 1:
+        if args.share_gpu:
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         world, rank = dist.get_world_size(), dist.get_rank()  # n_gpus from the live process group
     else:
         torch.cuda.set_device(0)
@@ -247,10 +255,11 @@ def main():
     gather_per_step = [a.elapsed_time(b) for a, b in events]
     gather_ms = float(np.mean(gather_per_step))
     if world > 1:
-        tt = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=dev)
+        cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, gather_ms = float(tt[0]), float(tt[1])
-        tot = torch.tensor([nseg_local], dtype=torch.int64, device=dev)
+        tot = torch.tensor([nseg_local], dtype=torch.int64, device=cdev)
         dist.all_reduce(tot)
         total_seg = int(tot.item())
     else:
