@@ -1,0 +1,45 @@
+"""CPU checks of bench.py's contract pieces that need no GPU: defaults (C2, 16 timed iterations, 2
+warmup, N = 1, strong packet-shard scaling), the roofline arithmetic and the host-thread count."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_defaults_are_the_c2_contract(bench):
+    a = bench.parse([])
+    assert (a.workload, a.steps, a.warmup, a.gpus) == ("c2", 16, 2, 1)
+    assert (a.photons, a.width, a.height, a.max_depth, a.radius, a.alpha) == (1_000_000, 512, 512, 5, 0.01, 0.5)
+    assert (a.scaling, a.shard_mode, a.pipeline, a.split, a.kernel) == ("strong", "packets", 1, 256, 0)
+    c5 = bench.parse(["--workload", "c5"])
+    assert (c5.steps, c5.photons, c5.width) == (10, 50_000_000, 1024)
+
+
+def test_roofline_fraction_is_achieved_over_peak(bench):
+    class WL:
+        def segments_per_gather(self):
+            return 1000
+
+    a = bench.parse(["--split", "4"])
+    st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000}
+    r = bench.roofline(st, a, WL(), 2.0, None, None)
+    items = (640 + 63) // 64 * 4
+    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 640 * 12 * (4 + 1)
+    assert r["algorithmic_bytes_per_launch"] == alg
+    assert r["achieved"] == pytest.approx(alg / 2e-3 / 1e9)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and r["unit"] == "GB/s" and r["traffic"] is None
+
+
+def test_host_threads_positive(bench):
+    n, note = bench.host_threads()
+    assert n >= 1 and "affinity" in note

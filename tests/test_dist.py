@@ -91,3 +91,21 @@ def test_two_rank_gloo_packet_shards_sum_to_single_rank(tmp_path, oracle, synth)
     ref = oracle.build(beams).gather(segs, R, npix=W * H)["accum"]
     assert np.abs(frame).max() > 0
     assert np.abs(frame - ref).max() <= 1e-6 * np.abs(ref).max()
+
+
+def test_packet_shards_partition_segments():
+    """libbre's bre_shard_segments (host arithmetic, no GPU) agrees with the host view of the packet
+    pick, and the shards' picks partition the segments -- including partial last packets / chunks,
+    more shards than chunks, and the argument errors (0 segments)."""
+    bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
+    for n in (0, 1, 63, 64, 65, 640, 1000, 4097, 64 * 37 + 5):
+        for count in (1, 2, 3, 8, 16):
+            for chunk in (1, 2, 4, 7):
+                parts = [bre.shard_packet_index(n, r, count, chunk) for r in range(count)]
+                for r, p in enumerate(parts):
+                    assert bre.shard_segments(n, r, count, chunk) == p.shape[0], (n, r, count, chunk)
+                    assert np.all(np.diff(p) > 0)
+                allseg = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+                assert np.array_equal(np.sort(allseg), np.arange(n)), (n, count, chunk)
+    assert bre.shard_segments(1000, 2, 2, 1) == 0 and bre.shard_segments(1000, -1, 2, 1) == 0
+    assert bre.shard_segments(1000, 0, 2, 0) == 0 and bre.shard_segments(-5, 0, 2, 1) == 0
