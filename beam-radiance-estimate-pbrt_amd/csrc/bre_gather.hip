@@ -45,7 +45,8 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
-// BRE_RMW_MAX_RUNS: exact-stage batches with more runs than this accumulate by LDS atomics
+// BRE_RMW_MAX_RUNS: exact-stage read-modify-write rounds per batch; a segment's pairs beyond this
+// many in one batch accumulate by LDS float atomics (tile_exact)
 #ifndef BRE_RMW_MAX_RUNS
 #define BRE_RMW_MAX_RUNS 8
 #endif
@@ -400,6 +401,7 @@ struct QEntry {
 struct TileShared {
     float4 tile[64][2];          // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
     float4 acc[64];              // per-segment RGB sums and contribution count (w, exact below 2^24)
+    int32_t rk[64];              // per-segment pair counter of the current exact batch
     QEntry q[kQueueCap + 64];    // prefilter survivors [0, t1), then one discard slot per lane
     int32_t stk[kStackDepth];
 };
@@ -457,34 +459,21 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
             contrib = true;
         }
     }
-    // Accumulate into the segments' LDS sums without atomics.  The batch is the queue in order: runs
-    // of one beam's pairs, each run in increasing segment lane (push), so the segment lanes inside a
-    // run are distinct.  Run by run, the run's contributing lanes read-modify-write their segment's
-    // float4 (one wave's LDS accesses are performed in order): each segment's terms are added in
-    // queue order.  (`count` only decides whether the count is used: it is always kept.)
+    // Accumulate into the segments' LDS sums in queue order.  An integer LDS atomic numbers each
+    // contributing pair among the batch's pairs of its segment (same-address lanes resolve in lane
+    // order, so rank = the pair's position among its segment's pairs in queue order); round k
+    // read-modify-writes the rank-k pairs, whose segments are distinct (one wave's LDS accesses are
+    // performed in order).  A batch takes as many rounds as its most repeated segment has pairs --
+    // at most its number of beam runs (a per-run loop took one round per run: 10% slower at C2).  Pairs of rank >= BRE_RMW_MAX_RUNS (a segment
+    // repeated along a transposed tile or a very coherent packet) add by LDS float atomics after the
+    // rounds, again in lane order.  (`count` only decides whether the count is used: it is always kept.)
     (void)count;
-    const unsigned long long cm = __ballot(contrib);
-    if (cm == 0ull) return;
-    const int prev = __shfl_up(e.beam, 1);
-    unsigned long long starts = __ballot(lane == 0 || e.beam != prev);
-    if (__popcll(starts) > BRE_RMW_MAX_RUNS) {
-        // many short runs (incoherent packets): one LDS float atomic per channel instead; lanes with
-        // the same address resolve in lane order, the same queue-order sum
-        if (contrib) {
-            atomicAdd(&sh.acc[sl].x, v.x);
-            atomicAdd(&sh.acc[sl].y, v.y);
-            atomicAdd(&sh.acc[sl].z, v.z);
-            atomicAdd(&sh.acc[sl].w, v.w);
-        }
-        return;
-    }
-    while (starts != 0ull) {
-        const int s0 = __ffsll((long long)starts) - 1;
-        starts &= starts - 1ull;
-        const unsigned long long upto = starts != 0ull ? (1ull << (__ffsll((long long)starts) - 1)) - 1ull : ~0ull;
-        const unsigned long long run = cm & upto & ~((1ull << s0) - 1ull);
-        if (run == 0ull) continue;
-        if ((run >> lane) & 1ull) {
+    if (__ballot(contrib) == 0ull) return;
+    sh.rk[lane] = 0;
+    const int rank = contrib ? atomicAdd(&sh.rk[sl], 1) : BRE_RMW_MAX_RUNS + 64;
+    for (int k = 0; k < BRE_RMW_MAX_RUNS; ++k) {
+        if (__ballot(rank == k) == 0ull) return;
+        if (rank == k) {
             float4 a = sh.acc[sl];
             a.x += v.x;
             a.y += v.y;
@@ -492,6 +481,12 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
             a.w += v.w;
             sh.acc[sl] = a;
         }
+    }
+    if (contrib & (rank >= BRE_RMW_MAX_RUNS)) {
+        atomicAdd(&sh.acc[sl].x, v.x);
+        atomicAdd(&sh.acc[sl].y, v.y);
+        atomicAdd(&sh.acc[sl].z, v.z);
+        atomicAdd(&sh.acc[sl].w, v.w);
     }
 }
 

@@ -1,0 +1,25 @@
+"""SHA-1 of one C2 / C3 iteration's gathered Ld from the libbre named by BRE_LIBRARY (bit-identity
+check of kernel variants): python ldhash.py c2|c3 ITER"""
+import hashlib
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.getcwd())
+bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
+sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
+wl, it = sys.argv[1], int(sys.argv[2])
+if wl == "c3":
+    scene, NPH, RES = sc.cornell_smoke_scene(0.5, 4.5, 0.7, n=64, seed=7), 5_000_000, 1024
+else:
+    scene, NPH, RES = sc.cornell_scene(0.05, 0.5, 0.0), 1_000_000, 512
+R = bre.beam_radius_at(0.01, 0.5, it)
+with bre.BeamGather(0) as g:
+    g.trace_photons(scene, NPH, it, 5, R)
+    g.camera_pass(scene, RES, RES, it, 5, True, True)
+    ld = torch.zeros((RES * RES, 3), dtype=torch.float32, device="cuda")
+    g.gather_camera(R, ld)
+    g.synchronize()
+print(wl, it, hashlib.sha1(ld.cpu().numpy().tobytes()).hexdigest(), float(ld.double().sum()))
