@@ -2,10 +2,10 @@
 # r2: exact-stage accumulation by per-segment rank (BRE_ACC_RANK 1) vs per-run RMW (production):
 # bit identity of one C2 iteration, then C2 / C3 throughput
 set -o pipefail
-O=gpurun_out/${EXPLORE_OUT:-explore40}; mkdir -p $O
+O=gpurun_out/${EXPLORE_OUT:-acc_rank}; mkdir -p $O
 V=beam-radiance-estimate-pbrt_amd/csrc/build/variants
 P=beam-radiance-estimate-pbrt_amd/libbre.so
-H=profiles/r2/explore/explore40/ldhash.py
+H=profiles/r2/explore/acc_rank/ldhash.py
 c2() { n=$1; lib=$2; shift 2
   BRE_LIBRARY=$lib timeout -k 10 300 python -u bench.py --no-cpu --no-pmc --no-diag --json-out $O/c2_$n.json "$@" > $O/c2_$n.log 2>&1 || { tail -n 20 $O/c2_$n.log; return 1; }
   python3 -c "import json;d=json.load(open('$O/c2_$n.json'));print('c2 $n', round(d['value']), 'ms/step', round(d['ms_per_step'],1))"

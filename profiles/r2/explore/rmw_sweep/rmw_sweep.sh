@@ -2,7 +2,7 @@
 # r2: exact-stage accumulation threshold BRE_RMW_MAX_RUNS (batches with more runs use LDS atomics):
 # 0 (always atomics), 4, 8 (production), 16, 64 (never atomics)
 set -o pipefail
-O=gpurun_out/${EXPLORE_OUT:-explore39}; mkdir -p $O
+O=gpurun_out/${EXPLORE_OUT:-rmw_sweep}; mkdir -p $O
 V=beam-radiance-estimate-pbrt_amd/csrc/build/variants
 c2() { n=$1; lib=$2; shift 2
   BRE_LIBRARY=$lib timeout -k 10 300 python -u bench.py --no-cpu --no-pmc --no-diag --json-out $O/c2_$n.json "$@" > $O/c2_$n.log 2>&1 || { tail -n 20 $O/c2_$n.log; return 1; }
