@@ -649,8 +649,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // against all kept beams at once (lane j: beam j), so a tile costs min(on lanes, kept beams)
         // steps.  Segment i's pairs are queued in beam order, exactly the order the beam-major scan
         // gives them, and every sum is a per-segment sum in queue order: bit-identical results.  The
-        // batches then hold one-pair runs (one beam each), so the exact stage accumulates them by its
-        // LDS-atomic path (or per run), both in queue order.
+        // batches then hold long stretches of one segment, whose ranks >= BRE_RMW_MAX_RUNS the exact
+        // stage adds by LDS atomics, in queue order like its rounds.
         const bool transposed = tscan > 0 && __popcll(onm) * 8 < __popcll(km) * tscan;
         if (BRE_SCAN_STATS) {
             const unsigned long long on = __popcll(onm), kp = __popcll(km);
