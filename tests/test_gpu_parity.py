@@ -435,3 +435,42 @@ def test_kernel4_dense_incoherent_is_deterministic(bre, synth, oracle, leaf):
     assert np.array_equal(runs[0]["counts"][:, 1], ref["contrib"])
     assert _seg_close(runs[0]["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
     assert np.array_equal(runs[0]["seg_rgb"], runs[1]["seg_rgb"])
+
+
+def test_segment_repeated_through_whole_batches(bre, oracle):
+    """A few segments, each crossed by ~1500 beams: the exact-stage batches hold up to 64 pairs of one
+    segment, so its accumulation runs all its read-modify-write rounds (ranks 0-7) and adds ranks
+    >= 8 by LDS atomics; the beam-major (tscan 0) and transposed (6) scans queue them alike.  Exact
+    contribution counts and sums to rounding against the oracle, bit-identical across the scans."""
+    rng = np.random.default_rng(11)
+    Rf, r = np.float32(0.02), np.float32(0.01)
+    axes = [(np.array([0.5, 0.5, 0.1], np.float32), np.array([0.0, 0.0, 1.0], np.float32)),
+            (np.array([0.2, 0.7, 0.3], np.float32), np.array([1.0, 0.0, 0.0], np.float32)),
+            (np.array([0.3, 0.1, 0.6], np.float32), np.array([0.0, 1.0, 0.0], np.float32))]
+    starts, ends = [], []
+    for o, d in axes:
+        m = 1500
+        c = o + d * rng.uniform(0.05, 0.75, m).astype(np.float32)[:, None]
+        e = np.cross(d, rng.normal(size=(m, 3))).astype(np.float32)
+        e /= np.linalg.norm(e, axis=1, keepdims=True)
+        c = (c + np.cross(d, e) * ((Rf + r) * rng.uniform(-0.5, 0.5, m)).astype(np.float32)[:, None]).astype(np.float32)
+        starts.append(c - e * np.float32(0.3))
+        ends.append(c + e * np.float32(0.3))
+    start, end = np.concatenate(starts).astype(np.float32), np.concatenate(ends).astype(np.float32)
+    beams = {"start": start, "end": end, "radius": np.full(len(start), r, np.float32),
+             "power": rng.random((len(start), 3), np.float32)}
+    o = np.stack([a[0] for a in axes]).astype(np.float32)
+    d = np.stack([a[1] for a in axes]).astype(np.float32)
+    segs = {"o": o, "p": (o + d * np.float32(0.8)).astype(np.float32), "d": d, "tmax": np.full(3, 0.8, np.float32)}
+    ref = oracle.build(beams).gather(segs, float(Rf))
+    assert ref["contrib"].min() > 500
+    outs = {}
+    for t in (0, 6):
+        with bre.BeamGather(0, counters=False, kernel=0) as g:
+            g.set_option(108, t)
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            outs[t] = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=float(Rf), counts=True)
+    out = outs[6]
+    assert np.array_equal(out["counts"][:, 1], ref["contrib"])
+    assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
+    assert np.array_equal(out["seg_rgb"], outs[0]["seg_rgb"])
