@@ -36,7 +36,7 @@ EXPORTS = [
     "bre_resolve_image", "bre_trace_photons", "bre_get_beams", "bre_scene_cornell", "bre_scene_cornell_smoke", "bre_smoke_density",
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
-    "bre_render_progressive", "bre_shard_segments",
+    "bre_render_progressive", "bre_shard_segments", "bre_set_beams_sharded", "bre_gather_sharded",
 ]
 
 
@@ -59,7 +59,8 @@ class Stats(ctypes.Structure):
                 ("n_photons", ctypes.c_int64),
                 ("photon_ms", ctypes.c_double),
                 ("n_camera_segments", ctypes.c_int64),
-                ("camera_ms", ctypes.c_double), ("n_chunks", ctypes.c_int64)]
+                ("camera_ms", ctypes.c_double), ("n_chunks", ctypes.c_int64),
+                ("queued_pairs", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -137,6 +138,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_render.restype = I32
     lib.bre_render_progressive.argtypes = [P, P, P, I32, P, P]
     lib.bre_render_progressive.restype = I32
+    lib.bre_set_beams_sharded.argtypes = [P, I32, I64, P, P, P, P]
+    lib.bre_set_beams_sharded.restype = I32
+    lib.bre_gather_sharded.argtypes = [P, I32, I64, P, P, P, P, P, F, I64, P, P, P]
+    lib.bre_gather_sharded.restype = I32
     _LIB = lib
     return lib
 
@@ -329,6 +334,44 @@ class BeamGather:
 
     def __exit__(self, *a):
         self.close()
+
+
+def _ctx_array(ctxs):
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    return arr
+
+
+def _check_group(ctxs, st):
+    if st != BRE_OK:
+        raise BreError(st, ctxs[0].lib.bre_last_error(ctxs[0].h).decode())
+
+
+def set_beams_sharded(ctxs, start, end, radius, power):
+    """bre_set_beams_sharded: the same beam set (host arrays) built on every context, in parallel."""
+    start, end, radius, power = (_f32(x) for x in (start, end, radius, power))
+    n = radius.shape[0]
+    _check_group(ctxs, ctxs[0].lib.bre_set_beams_sharded(_ctx_array(ctxs), len(ctxs), n, _ptr(start), _ptr(end),
+                                                         _ptr(radius), _ptr(power)))
+
+
+def gather_sharded(ctxs, o, p, d, tmax, pixel=None, R=0.01, npix=0, accum=None, seg_rgb=True, counts=False):
+    """bre_gather_sharded over BeamGather contexts (one per GPU): host arrays, as BeamGather.gather."""
+    o, p, d, tmax = (_f32(x) for x in (o, p, d, tmax))
+    n = tmax.shape[0]
+    pix = None if pixel is None else np.ascontiguousarray(pixel, dtype=np.int32)
+    out = np.zeros((n, 3), np.float32) if seg_rgb else None
+    cnt = np.zeros((n, 2), np.int32) if counts else None
+    if accum is not None:
+        assert accum.dtype == np.float32 and accum.flags.c_contiguous
+    _check_group(ctxs, ctxs[0].lib.bre_gather_sharded(_ctx_array(ctxs), len(ctxs), n, _ptr(o), _ptr(p), _ptr(d),
+                                                      _ptr(tmax), _ptr(pix), float(R), int(npix), _ptr(accum),
+                                                      _ptr(out), _ptr(cnt)))
+    res = {}
+    if out is not None:
+        res["seg_rgb"] = out
+    if cnt is not None:
+        res["counts"] = cnt
+    return res
 
 
 def shard_segments(n_segments: int, rank: int, count: int, chunk: int = 1) -> int:

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bre.h"
@@ -69,6 +70,7 @@ struct bre_ctx {
     int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
+    int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
     int chunk_len = 400;   // chunk length in units of E / 100
@@ -415,26 +417,54 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         return gather_chunk(c, a);
     }
     if (kernel == 0) kernel = 4;  // the tile kernel on the tile tree built for kernel 0
-    if (kernel == 4) {
-        HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
-        HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)nseg * (size_t)c->split));
-        if (c->roots_split != c->split) {
-            HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
-            c->roots_split = c->split;
-        }
-        a.roots = c->roots.as<int32_t>();
-        a.partial = c->partial.as<float>();
-        HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)((nseg + 63) / 64 * 64)));  // whole packets
-        a.segrec = c->segrec.as<SegRec>();
-        if (c->counters || seg_counts) {
-            HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)nseg * (size_t)c->split));
-            a.pcnt = c->pcnt.as<int32_t>();
-        }
-    } else if (kernel == 2 && seg_index) {
-        return fail(c, BRE_ERR_STATE, "kernel 2 gathers in the caller's order only");
+    if (kernel == 2 && seg_index) return fail(c, BRE_ERR_STATE, "kernel 2 gathers in the caller's order only");
+    if (kernel == 2) {
+        if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+        HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
+        if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+        return read_counters(c, a.ctr);
+    }
+    // The tile kernel keeps S partial sums per segment (12 B each, + 8 B of counts when asked for).
+    // A gather of many segments runs as consecutive launches over whole-packet ranges, so that the
+    // partials stay within partial_cap (4 GiB: C2's ~0.6M segments in one launch, C4's ~9.6M in 7)
+    // and the grid within HIP's 2^32 work items.  Every segment's sum is still its subtrees'
+    // partials added in root order by k_reduce: the per-segment results do not depend on the split.
+    const bool want_cnt = c->counters || seg_counts;
+    const size_t per_seg = (size_t)c->split * (12 + (want_cnt ? 8 : 0));
+    int64_t chunk = c->partial_cap / (int64_t)per_seg / 64 * 64;
+    if (chunk < 64) chunk = 64;
+    if (chunk > nseg) chunk = nseg;
+    HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
+    HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)chunk * (size_t)c->split));
+    if (c->roots_split != c->split) {
+        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
+        c->roots_split = c->split;
+    }
+    a.roots = c->roots.as<int32_t>();
+    a.partial = c->partial.as<float>();
+    HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)((chunk + 63) / 64 * 64)));  // whole packets
+    a.segrec = c->segrec.as<SegRec>();
+    if (want_cnt) {
+        HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)chunk * (size_t)c->split));
+        a.pcnt = c->pcnt.as<int32_t>();
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-    HIPCHK(c, launch_gather(a, kernel, c->counters, c->stream));
+    for (int64_t off = 0; off < nseg; off += chunk) {
+        GatherArgs ac = a;
+        ac.nseg = std::min(chunk, nseg - off);
+        ac.o = o + 3 * off;
+        ac.p = p + 3 * off;
+        ac.d = d + 3 * off;
+        ac.tmax = tmax + off;
+        ac.pixel = pixel ? pixel + off : nullptr;
+        if (seg_index) {
+            ac.seg_index = seg_index + off;  // outputs are addressed through the index
+        } else {
+            ac.seg_rgb = seg_rgb ? seg_rgb + 3 * off : nullptr;
+            ac.seg_counts = seg_counts ? seg_counts + 2 * off : nullptr;
+        }
+        HIPCHK(c, launch_gather(ac, kernel, c->counters, c->stream));
+    }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
     return read_counters(c, a.ctr);
 }
@@ -460,6 +490,7 @@ bre_status read_counters(bre_ctx *c, DevCounters *ctr) {
     c->stats.useful_beam_evals = (int64_t)h.useful_beam_evals;
     c->stats.max_stack_depth = (int64_t)h.max_stack;
     c->stats.redo_items = 0;
+    c->stats.queued_pairs = (int64_t)h.queued_pairs;
     c->stats.n_chunks = c->n_chunks;
     return check_flags(c);
 }
@@ -592,6 +623,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
+    case 109:  // internal: tile kernel partial-sum bytes per launch, in MiB (tests force several launches)
+        if (value < 1 || value > ((int64_t)1 << 20)) return fail(c, BRE_ERR_INVALID_ARG, "partial cap must be in 1..2^20 MiB");
+        c->partial_cap = value << 20;
+        return BRE_OK;
     case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated (sweeps)
         if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0..3");
         c->block_map = (int)value;
@@ -734,6 +769,9 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     if (st != BRE_OK) return st;
     st = set_device(c);
     if (st != BRE_OK) return st;
+    // an earlier asynchronous gather's device errors are reported before this call changes anything
+    st = check_flags(c);
+    if (st != BRE_OK) return st;
     st = upload_scene(c, scene);
     if (st != BRE_OK) return st;
     const size_t N = (size_t)n_photons;
@@ -772,13 +810,11 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     st = build(c, total, c->in_start.as<float>(), c->in_end.as<float>(), c->in_radius.as<float>(),
                c->in_power.as<float>());
     if (st != BRE_OK) return st;
-    st = check_flags(c);  // also reports an earlier asynchronous gather's device errors
-    if (st != BRE_OK) return st;
     c->beams_kept = true;
     c->stats.n_photons = n_photons;
     c->stats.photon_ms = photon_ms;
     if (n_beams) *n_beams = total;
-    return BRE_OK;
+    return check_flags(c);
 }
 
 bre_status bre_get_beams(bre_ctx *c, int64_t capacity, float *start, float *end, float *radius, float *power,
@@ -817,6 +853,8 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     st = check_medium(c, scene, "bre_camera_pass");
     if (st != BRE_OK) return st;
     st = set_device(c);
+    if (st != BRE_OK) return st;
+    st = check_flags(c);  // an earlier gather's device errors, before this pass changes anything
     if (st != BRE_OK) return st;
     // scene + camera/Halton tables (rebuilt when the scene or film changes)
     st = upload_scene(c, scene);
@@ -883,32 +921,45 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
         HIPCHK(c, hipEventSynchronize(c->ev[1]));
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     }
-    st = check_flags(c);
-    if (st != BRE_OK) return st;
     c->cam_nseg = n;
     c->cam_npix = (int64_t)width * height;
     c->stats.n_camera_segments = n;
     c->stats.camera_ms = ms;
     if (n_segments) *n_segments = n;
-    return BRE_OK;
+    return check_flags(c);
 }
 
-// The camera segments of the last camera pass against the beam set, in the production order: the
-// segments only add into their pixels, so the packet kernel takes them in a coherence order
-// (bre_sort.hip); per-segment outputs (optional) are scattered back to the camera-pass order.
-static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_seg_rgb, int32_t *d_seg_counts) {
-    if (c->cam_npix == 0) return fail(c, BRE_ERR_STATE, "bre_gather_camera: no camera pass yet");
-    bre_status st = set_device(c);
-    if (st != BRE_OK) return st;
-    const int64_t n = c->cam_nseg;
-    // packet sharding (BRE_OPT_SHARD_MODE 1): this rank gathers the chunks c = rank (mod count) of
-    // BRE_OPT_SHARD_BLOCK consecutive 64-segment packets of the (sorted) order, copied into contiguous
-    // arrays first (bre_shard_segments)
+// n device segments against the beam set in the production order: the segments only add into
+// their pixels, so the packet kernel takes them in a coherence order (bre_sort.hip; kernels 0 / 4);
+// per-segment outputs (optional) are scattered back to the caller's order.  Under
+// BRE_OPT_SHARD_MODE 1 with a shard count > 1 only this shard's packets of that order are gathered
+// (bre_shard_segments): the other entries of the per-segment outputs are zeroed, and the shards'
+// films and outputs sum to the one-shard results.  Used by bre_gather_camera (the camera pass's
+// segments), bre_gather_device and bre_gather (the caller's segments).
+static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const float *p, const float *d,
+                                  const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
+                                  float *d_seg_rgb, int32_t *d_seg_counts) {
     const bool pshard = c->shard_mode == 1 && c->shard_count > 1;
     const bool sortable = c->kernel == 0 || c->kernel == 4;  // kernels 2 / 5 write in the caller's order
+    const bool seg_out = d_seg_rgb || d_seg_counts;
+    if (n < 0 || npix < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: negative size");
+    if (n > 0 && (!o || !p || !d || !t)) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: null segment array");
+    if (d_accum && !pix) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: accum_rgb given without seg_pixel");
+    if (pshard && seg_out) {
+        if (!sortable) return fail(c, BRE_ERR_STATE, "packet shards with per-segment outputs need kernel 0 or 4");
+        // every entry is defined: the other shards' segments read 0 here
+        GatherArgs z{};
+        z.nseg = n;
+        z.seg_rgb = d_seg_rgb;
+        z.seg_counts = d_seg_counts;
+        HIPCHK(c, launch_zero_outputs(z, c->stream));
+    }
+    // packet sharding: this shard gathers the chunks c = rank (mod count) of BRE_OPT_SHARD_BLOCK
+    // consecutive 64-segment packets of the (sorted) order, copied into contiguous arrays first
     const auto pick = [&](const float *o, const float *p, const float *d, const float *t, const int32_t *pix,
                           const int32_t *index) -> bre_status {
         const int64_t m = bre_shard_segments(n, c->shard_rank, c->shard_count, c->shard_block);
+        c->stats.n_segments = m;
         if (m == 0) return BRE_OK;
         const size_t M = (size_t)m;
         HIPCHK(c, c->sp_o.ensure(M * 3 * sizeof(float)));
@@ -916,26 +967,18 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
         HIPCHK(c, c->sp_d.ensure(M * 3 * sizeof(float)));
         HIPCHK(c, c->sp_t.ensure(M * sizeof(float)));
         HIPCHK(c, c->sp_pix.ensure(M * sizeof(int32_t)));
-        const bool want_index = d_seg_rgb || d_seg_counts;
-        if (want_index) HIPCHK(c, c->sp_index.ensure(M * sizeof(int32_t)));
+        if (seg_out) HIPCHK(c, c->sp_index.ensure(M * sizeof(int32_t)));
         HIPCHK(c, launch_packet_pick(n, m, c->shard_rank, c->shard_count, c->shard_block, o, p, d, t, pix, index,
                                      c->sp_o.as<float>(), c->sp_p.as<float>(), c->sp_d.as<float>(),
                                      c->sp_t.as<float>(), c->sp_pix.as<int32_t>(),
-                                     want_index ? c->sp_index.as<int32_t>() : nullptr, c->stream));
+                                     seg_out ? c->sp_index.as<int32_t>() : nullptr, c->stream));
         return gather_device(c, m, c->sp_o.as<float>(), c->sp_p.as<float>(), c->sp_d.as<float>(),
-                             c->sp_t.as<float>(), c->sp_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
-                             d_seg_counts, want_index ? c->sp_index.as<int32_t>() : nullptr);
+                             c->sp_t.as<float>(), pix ? c->sp_pix.as<int32_t>() : nullptr, R, npix, d_accum,
+                             d_seg_rgb, d_seg_counts, seg_out ? c->sp_index.as<int32_t>() : nullptr);
     };
-    if (!c->sort_segments || n < 2 || (!sortable && (d_seg_rgb || d_seg_counts))) {
-        if (pshard) {
-            if (!sortable && (d_seg_rgb || d_seg_counts))
-                return fail(c, BRE_ERR_STATE, "packet shards with per-segment outputs need kernel 0 or 4");
-            return pick(c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(), c->seg_t.as<float>(),
-                        c->seg_pix.as<int32_t>(), nullptr);
-        }
-        return gather_device(c, n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
-                             c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
-                             d_seg_counts);
+    if (!c->sort_segments || n < 2 || (!sortable && seg_out)) {
+        if (pshard) return pick(o, p, d, t, pix, nullptr);
+        return gather_device(c, n, o, p, d, t, pix, R, npix, d_accum, d_seg_rgb, d_seg_counts);
     }
     const size_t N = (size_t)n;
     HIPCHK(c, c->ss_bounds.ensure(8 * sizeof(unsigned int)));
@@ -950,16 +993,25 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
     HIPCHK(c, c->ss_d.ensure(N * 3 * sizeof(float)));
     HIPCHK(c, c->ss_t.ensure(N * sizeof(float)));
     HIPCHK(c, c->ss_pix.ensure(N * sizeof(int32_t)));
-    SegSort ss{n, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(), c->seg_t.as<float>(),
-               c->seg_pix.as<int32_t>(), c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
+    SegSort ss{n, o, p, d, t, pix, c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
                c->ss_keys_alt.as<unsigned long long>(), c->ss_vals.as<int32_t>(), c->ss_vals_alt.as<int32_t>(),
                c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
                c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
-    // ss_vals_alt[i] = the camera-pass index of sorted segment i (the sort's permutation)
+    // ss_vals_alt[i] = the caller's index of sorted segment i (the sort's permutation)
     if (pshard) return pick(ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, c->ss_vals_alt.as<int32_t>());
-    return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, R, c->cam_npix, d_accum, d_seg_rgb, d_seg_counts,
-                         (d_seg_rgb || d_seg_counts) ? c->ss_vals_alt.as<int32_t>() : nullptr);
+    return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, pix ? ss.pix2 : nullptr, R, npix, d_accum, d_seg_rgb,
+                         d_seg_counts, seg_out ? c->ss_vals_alt.as<int32_t>() : nullptr);
+}
+
+// The camera segments of the last camera pass against the beam set (gather_segments).
+static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_seg_rgb, int32_t *d_seg_counts) {
+    if (c->cam_npix == 0) return fail(c, BRE_ERR_STATE, "bre_gather_camera: no camera pass yet");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    return gather_segments(c, c->cam_nseg, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
+                           c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
+                           d_seg_counts);
 }
 
 bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {
@@ -1188,7 +1240,7 @@ bre_status bre_gather_device(bre_ctx *c, int64_t nseg, const float *o, const flo
     if (!c) return BRE_ERR_INVALID_ARG;
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
-    return gather_device(c, nseg, o, p, d, tmax, pixel, R, npix, accum, seg_rgb, seg_counts);
+    return gather_segments(c, nseg, o, p, d, tmax, pixel, R, npix, accum, seg_rgb, seg_counts);
 }
 
 bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
@@ -1238,13 +1290,116 @@ bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, 
         HIPCHK(c, c->g_counts.ensure(S * 2 * sizeof(int32_t)));
         dcnt = c->g_counts.as<int32_t>();
     }
-    st = gather_device(c, nseg, c->g_o.as<float>(), c->g_p.as<float>(), c->g_d.as<float>(), c->g_tmax.as<float>(), dpix,
-                       R, npix, daccum, dseg, dcnt);
+    st = gather_segments(c, nseg, c->g_o.as<float>(), c->g_p.as<float>(), c->g_d.as<float>(), c->g_tmax.as<float>(),
+                         dpix, R, npix, daccum, dseg, dcnt);
     if (st != BRE_OK) return st;
     if (daccum) HIPCHK(c, hipMemcpyAsync(accum, daccum, P * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (dseg) HIPCHK(c, hipMemcpyAsync(seg_rgb, dseg, S * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (dcnt) HIPCHK(c, hipMemcpyAsync(seg_counts, dcnt, S * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     return check_flags(c);
+}
+
+}  // extern "C"
+
+// ---- multi-GPU: one host thread per context ----
+namespace {
+struct ShardSave {
+    int mode, count, rank, block;
+};
+// Run fn(i) for every context on its own thread (fn(0) on the caller's); the first failing
+// context's status and message (prefixed with its index) end up in ctxs[0].
+template <typename Fn>
+bre_status for_each_ctx(bre_ctx *const *ctxs, int n, Fn fn) {
+    std::vector<bre_status> st((size_t)n, BRE_OK);
+    std::vector<std::thread> th;
+    th.reserve((size_t)n);
+    for (int i = 1; i < n; ++i) th.emplace_back([&, i] { st[(size_t)i] = fn(i); });
+    st[0] = fn(0);
+    for (auto &t : th) t.join();
+    for (int i = 0; i < n; ++i) {
+        if (st[(size_t)i] == BRE_OK) continue;
+        const std::string msg = "context " + std::to_string(i) + ": " + ctxs[i]->err;
+        ctxs[0]->err = msg;
+        return st[(size_t)i];
+    }
+    return BRE_OK;
+}
+bre_status check_ctxs(bre_ctx *const *ctxs, int n) {
+    if (!ctxs || n < 1) return BRE_ERR_INVALID_ARG;
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return BRE_ERR_INVALID_ARG;
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return fail(ctxs[0], BRE_ERR_INVALID_ARG, "bre_*_sharded: context %d repeated", i);
+    }
+    return BRE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+bre_status bre_set_beams_sharded(bre_ctx *const *ctxs, int n_ctx, int64_t n, const float *start, const float *end,
+                                 const float *radius, const float *power) {
+    bre_status st = check_ctxs(ctxs, n_ctx);
+    if (st != BRE_OK) return st;
+    return for_each_ctx(ctxs, n_ctx, [&](int i) { return bre_set_beams(ctxs[i], n, start, end, radius, power); });
+}
+
+bre_status bre_gather_sharded(bre_ctx *const *ctxs, int n_ctx, int64_t nseg, const float *o, const float *p,
+                              const float *d, const float *tmax, const int32_t *pixel, float R, int64_t npix,
+                              float *accum, float *seg_rgb, int32_t *seg_counts) {
+    bre_status st = check_ctxs(ctxs, n_ctx);
+    if (st != BRE_OK) return st;
+    if (nseg < 0 || npix < 0) return fail(ctxs[0], BRE_ERR_INVALID_ARG, "bre_gather_sharded: negative size");
+    const size_t F = accum && npix > 0 ? (size_t)npix * 3 : 0, S = (size_t)nseg;
+    // per context: its partial film and per-segment outputs (only its own packets' entries are
+    // nonzero); the contexts' shard options are set for the call and restored afterwards
+    std::vector<std::vector<float>> film((size_t)n_ctx), rgb((size_t)n_ctx);
+    std::vector<std::vector<int32_t>> cnt((size_t)n_ctx);
+    std::vector<ShardSave> saved((size_t)n_ctx);
+    for (int i = 0; i < n_ctx; ++i) {
+        bre_ctx *c = ctxs[i];
+        saved[(size_t)i] = ShardSave{c->shard_mode, c->shard_count, c->shard_rank, c->shard_block};
+        c->shard_mode = 1;
+        c->shard_count = n_ctx;
+        c->shard_rank = i;
+        c->shard_block = 1;
+    }
+    st = for_each_ctx(ctxs, n_ctx, [&](int i) {
+        const size_t k = (size_t)i;
+        film[k].assign(F, 0.f);
+        if (seg_rgb) rgb[k].assign(S * 3, 0.f);
+        if (seg_counts) cnt[k].assign(S * 2, 0);
+        return bre_gather(ctxs[i], nseg, o, p, d, tmax, pixel, R, npix, F ? film[k].data() : nullptr,
+                          seg_rgb ? rgb[k].data() : nullptr, seg_counts ? cnt[k].data() : nullptr);
+    });
+    for (int i = 0; i < n_ctx; ++i) {
+        bre_ctx *c = ctxs[i];
+        const ShardSave &v = saved[(size_t)i];
+        c->shard_mode = v.mode;
+        c->shard_count = v.count;
+        c->shard_rank = v.rank;
+        c->shard_block = v.block;
+    }
+    if (st != BRE_OK) return st;
+    // the films in context order (deterministic), then into the caller's Ld
+    for (size_t j = 0; j < F; ++j) {
+        float v = film[0][j];
+        for (int i = 1; i < n_ctx; ++i) v += film[(size_t)i][j];
+        accum[j] += v;
+    }
+    if (seg_rgb)
+        for (size_t j = 0; j < S * 3; ++j) {
+            float v = rgb[0][j];
+            for (int i = 1; i < n_ctx; ++i) v += rgb[(size_t)i][j];  // one nonzero term per entry
+            seg_rgb[j] = v;
+        }
+    if (seg_counts)
+        for (size_t j = 0; j < S * 2; ++j) {
+            int32_t v = cnt[0][j];
+            for (int i = 1; i < n_ctx; ++i) v += cnt[(size_t)i][j];
+            seg_counts[j] = v;
+        }
+    return BRE_OK;
 }
 
 int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int32_t chunk) {

@@ -299,7 +299,7 @@ __device__ __forceinline__ void eval_chunk(const Lane &L, const ChunkV &c, int64
     acc.r += pv.x * wgt;
     acc.g += pv.y * wgt;
     acc.b += pv.z * wgt;
-    if (COUNT) ++acc.contrib;
+    ++acc.contrib;  // always: seg_counts[1] is defined without counters too (C = -1 then)
 }
 
 template <bool COUNT, bool PREF>
@@ -391,8 +391,8 @@ __global__ __launch_bounds__(kChunkBlock) void k_gather_chunk(
                 atomicAdd(&accum[3 * (int64_t)px + 2], acc.b);
             }
         }
-        if (COUNT && seg_counts) {
-            seg_counts[2 * s] = acc.ccp;
+        if (seg_counts) {
+            seg_counts[2 * s] = COUNT ? acc.ccp : -1;
             seg_counts[2 * s + 1] = acc.contrib;
         }
     }

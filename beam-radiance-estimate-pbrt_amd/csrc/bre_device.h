@@ -52,7 +52,7 @@ struct DevCounters {
     unsigned long long ccp_wave_evals;     // exact-stage batches of <= 64 pairs (per wave)
     unsigned long long prefilter_rejects;  // lane-level candidate rejects by the line-distance prefilters
     unsigned long long useful_beam_evals;  // beams kept by the packet bundle test
-    unsigned long long redo_items;         // unused (kept for the stats layout)
+    unsigned long long queued_pairs;       // tile kernel, counters: (lane, beam) pairs queued for the exact stage
     unsigned int max_stack;
     unsigned int flags;  // kFlag* bits (sticky)
 };

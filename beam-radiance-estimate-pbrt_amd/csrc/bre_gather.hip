@@ -81,7 +81,7 @@ __device__ __forceinline__ unsigned long long phase_clock() {
 }
 
 struct Prof {
-    unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0;
+    unsigned long long leaves = 0, beams = 0, ccp_waves = 0, rejects = 0, useful = 0, queued = 0;
 };
 
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
@@ -560,6 +560,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
         sh.q[need ? rank : kQueueCap + lane] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
+        if (COUNT) pf.queued += __popcll(m);
         if (BRE_SCAN_STATS) ss_q += __popcll(m);
     };
     // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan),
@@ -850,6 +851,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             atomicAdd(&ctr->useful_beam_evals, pf.useful);
             atomicAdd(&ctr->prefilter_rejects, rj);
             atomicAdd(&ctr->ccp_wave_evals, pf.ccp_waves);
+            atomicAdd(&ctr->queued_pairs, pf.queued);
         }
     }
 }
@@ -1062,9 +1064,11 @@ __global__ __launch_bounds__(kThreadBlock) void k_gather_thread(
     finish_lane<COUNT>(s, valid, cr, cg, cb, cand, contrib, visits, pixel, npix, accum, seg_rgb, seg_counts, ctr);
 }
 
-__global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *__restrict__ seg_counts) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= nseg) return;
+__global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *__restrict__ seg_counts,
+                           const int32_t *__restrict__ seg_index) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nseg) return;
+    const int64_t s = seg_index ? (int64_t)seg_index[i] : i;  // the caller's entry of gathered segment i
     if (seg_rgb) {
         seg_rgb[3 * s] = 0.f;
         seg_rgb[3 * s + 1] = 0.f;
@@ -1140,7 +1144,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
 hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s) {
     if (a.nseg == 0 || (!a.seg_rgb && !a.seg_counts)) return hipSuccess;
     hipLaunchKernelGGL(k_zero_seg, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.seg_rgb,
-                       a.seg_counts);
+                       a.seg_counts, a.seg_index);
     return hipGetLastError();
 }
 

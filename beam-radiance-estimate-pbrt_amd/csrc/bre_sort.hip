@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t
         d2[3 * i + k] = d[3 * j + k];
     }
     t2[i] = t[j];
-    pix2[i] = pix[j];
+    pix2[i] = pix ? pix[j] : 0;  // no pixel array: a gather without a film (per-segment outputs only)
 }
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, in
         d2[3 * j + k] = d[3 * src + k];
     }
     t2[j] = t[src];
-    pix2[j] = pix[src];
+    pix2[j] = pix ? pix[src] : 0;
     if (index2) index2[j] = index ? index[src] : (int32_t)src;
     (void)n;
 }

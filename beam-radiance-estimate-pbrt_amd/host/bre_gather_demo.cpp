@@ -1,15 +1,17 @@
 // bre_gather_demo.cpp — C++ host program using the integrator mirror (photonbeam_gpu.h) the way
 // adapters/pbrt/photonbeam.patch does: build the iteration's beams (PhotonBeamGpuBVH::Build,
 // photonbeam.cpp:438), record camera segments in per-thread SegmentRecorders (:494-508), one
-// Gather per recorder into the pixel Ld buffer, ResolveImage (:578).
+// batched Gather of all recorders into the pixel Ld buffer, ResolveImage (:578).
 //
 //   bre_gather_demo [W]                      built-in lattice scene, prints the image sum
-//   bre_gather_demo --beams B --segments S --out O [--split K] [--iteration I]
+//   bre_gather_demo --beams B --segments S --out O [--split K] [--iteration I] [--devices D]
 //       B: int64 n, then n x {start xyz, end xyz, radius, powerEnd rgb} float32
 //       S: int64 n, int64 nPixels, float32 R, then n x {o xyz, p xyz, d xyz, tMax} float32 + int32 pixel
 //       O: nPixels x rgb float32, the resolved image L = Ld / (I + 1)
 //       K: number of recorders the segments are dealt to round-robin (the patch's per-thread
-//          recorders), each gathered with its own call
+//          recorders), all gathered in one call
+//       D: GPU ordinals separated by commas, one libbre context each (e.g. 0,1,2,3; 0,0,0 puts three
+//          contexts on GPU 0): the beams are replicated and the segment packets split over them
 // Exit code 0 on success, 1 on a libbre or IO error, 2 without a GPU.
 #include <cmath>
 #include <cstdio>
@@ -29,7 +31,8 @@ bool ReadAll(FILE *f, T *dst, size_t n) {
     return std::fread(dst, sizeof(T), n, f) == n;
 }
 
-int FileMode(const char *beamsPath, const char *segPath, const char *outPath, int split, int iteration) {
+int FileMode(const char *beamsPath, const char *segPath, const char *outPath, int split, int iteration,
+             const std::vector<int> &devices) {
     FILE *fb = std::fopen(beamsPath, "rb");
     FILE *fs = std::fopen(segPath, "rb");
     if (!fb || !fs) {
@@ -74,7 +77,7 @@ int FileMode(const char *beamsPath, const char *segPath, const char *outPath, in
     std::fclose(fb);
     std::fclose(fs);
 
-    PhotonBeamGpuBVH bvh(0);
+    PhotonBeamGpuBVH bvh(devices);
     if (!bvh.Ok()) {
         std::fprintf(stderr, "no GPU: %s\n", bvh.LastError().c_str());
         return 2;
@@ -84,11 +87,10 @@ int FileMode(const char *beamsPath, const char *segPath, const char *outPath, in
         return 1;
     }
     std::vector<float> ld(3 * (size_t)npix, 0.f);
-    for (const auto &r : recorders)
-        if (r.Size() && !bvh.Gather(r, R, ld)) {
-            std::fprintf(stderr, "gather: %s\n", bvh.LastError().c_str());
-            return 1;
-        }
+    if (!bvh.Gather(recorders, R, ld)) {
+        std::fprintf(stderr, "gather: %s\n", bvh.LastError().c_str());
+        return 1;
+    }
     std::vector<float> rgb;
     ResolveImage(ld, iteration, rgb);
     FILE *fo = std::fopen(outPath, "wb");
@@ -99,8 +101,9 @@ int FileMode(const char *beamsPath, const char *segPath, const char *outPath, in
     std::fclose(fo);
     bre_stats st;
     if (bvh.Stats(&st))
-        std::printf("bre_gather_demo: %lld beams, %lld segments in %zu gathers, %lld nodes\n", (long long)nb,
-                    (long long)ns, recorders.size(), (long long)st.n_nodes);
+        std::printf("bre_gather_demo: %lld beams, %lld segments from %zu recorders in one gather on %d contexts, "
+                    "%lld nodes\n", (long long)nb, (long long)ns, recorders.size(), bvh.Devices(),
+                    (long long)st.n_nodes);
     return 0;
 }
 
@@ -160,6 +163,7 @@ int LatticeMode(int W) {
 int main(int argc, char **argv) {
     const char *beams = nullptr, *segs = nullptr, *out = nullptr;
     int split = 1, iteration = 0;
+    std::vector<int> devices{0};
     for (int i = 1; i < argc; ++i) {
         const bool more = i + 1 < argc;
         if (!std::strcmp(argv[i], "--beams") && more) beams = argv[++i];
@@ -167,10 +171,19 @@ int main(int argc, char **argv) {
         else if (!std::strcmp(argv[i], "--out") && more) out = argv[++i];
         else if (!std::strcmp(argv[i], "--split") && more) split = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--iteration") && more) iteration = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--devices") && more) {
+            devices.clear();
+            for (const char *q = argv[++i]; *q;) {
+                char *e = nullptr;
+                devices.push_back((int)std::strtol(q, &e, 10));
+                if (e == q) break;
+                q = *e == ',' ? e + 1 : e;
+            }
+        }
         else if (argv[i][0] != '-' && !beams) return LatticeMode(std::atoi(argv[i]));
         else {
             std::fprintf(stderr, "usage: bre_gather_demo [W] | --beams B --segments S --out O [--split K] "
-                                 "[--iteration I]\n");
+                                 "[--iteration I] [--devices D0,D1,..]\n");
             return 1;
         }
     }
@@ -179,7 +192,7 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "bre_gather_demo: --beams, --segments and --out go together\n");
             return 1;
         }
-        return FileMode(beams, segs, out, split, iteration);
+        return FileMode(beams, segs, out, split, iteration, devices);
     }
     return LatticeMode(64);
 }

@@ -2,6 +2,7 @@
 #include "photonbeam_gpu.h"
 
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 namespace bre_host {
@@ -22,31 +23,65 @@ void SegmentRecorder::Record(const CameraSegment &s) {
     pixel_.push_back(s.pixel);
 }
 
-PhotonBeamGpuBVH::PhotonBeamGpuBVH(int device) {
-    bre_status st = bre_create(device, &ctx_);
-    if (st != BRE_OK) {
-        ctx_ = nullptr;
-        err_ = "bre_create failed with status " + std::to_string((int)st);
-    }
+void SegmentRecorder::Append(const SegmentRecorder &other) {
+    o_.insert(o_.end(), other.o_.begin(), other.o_.end());
+    p_.insert(p_.end(), other.p_.begin(), other.p_.end());
+    d_.insert(d_.end(), other.d_.begin(), other.d_.end());
+    tmax_.insert(tmax_.end(), other.tmax_.begin(), other.tmax_.end());
+    pixel_.insert(pixel_.end(), other.pixel_.begin(), other.pixel_.end());
 }
 
-PhotonBeamGpuBVH::~PhotonBeamGpuBVH() { bre_destroy(ctx_); }
+std::vector<int> DevicesFromEnv() {
+    std::vector<int> out;
+    const char *e = std::getenv("BRE_DEVICES");
+    for (const char *q = e ? e : ""; *q;) {
+        char *end = nullptr;
+        const long v = std::strtol(q, &end, 10);
+        if (end == q) break;
+        out.push_back((int)v);
+        q = *end == ',' ? end + 1 : end;
+    }
+    if (out.empty()) out.push_back(0);
+    return out;
+}
+
+PhotonBeamGpuBVH::PhotonBeamGpuBVH(int device) : PhotonBeamGpuBVH(std::vector<int>{device}) {}
+
+PhotonBeamGpuBVH::PhotonBeamGpuBVH(const std::vector<int> &devices) {
+    if (devices.empty()) err_ = "no device given";
+    for (int dev : devices) {
+        bre_ctx *c = nullptr;
+        const bre_status st = bre_create(dev, &c);
+        if (st != BRE_OK) {
+            err_ = "bre_create(" + std::to_string(dev) + ") failed with status " + std::to_string((int)st);
+            break;
+        }
+        ctx_.push_back(c);
+    }
+    ready_ = !devices.empty() && ctx_.size() == devices.size();
+}
+
+PhotonBeamGpuBVH::~PhotonBeamGpuBVH() {
+    for (bre_ctx *c : ctx_) bre_destroy(c);
+}
 
 bool PhotonBeamGpuBVH::Check(bre_status st) {
     if (st == BRE_OK) return true;
-    err_ = ctx_ ? bre_last_error(ctx_) : "no context";
+    err_ = ctx_.empty() ? "no context" : bre_last_error(ctx_[0]);
     return false;
 }
 
 bool PhotonBeamGpuBVH::SetOption(bre_option opt, int64_t value) {
-    if (!ctx_) return false;
-    return Check(bre_set_option(ctx_, opt, value));
+    if (!Ok()) return false;
+    for (bre_ctx *c : ctx_)
+        if (!Check(bre_set_option(c, opt, value))) return false;
+    return true;
 }
 
-bool PhotonBeamGpuBVH::Stats(bre_stats *out) const { return ctx_ && bre_get_stats(ctx_, out) == BRE_OK; }
+bool PhotonBeamGpuBVH::Stats(bre_stats *out) const { return Ok() && bre_get_stats(ctx_[0], out) == BRE_OK; }
 
 bool PhotonBeamGpuBVH::Build(const std::vector<PhotonBeam> &beams) {
-    if (!ctx_) return false;
+    if (!Ok()) return false;
     const size_t n = beams.size();
     std::vector<float> s(3 * n), e(3 * n), r(n), pw(3 * n);
     for (size_t i = 0; i < n; ++i) {
@@ -56,14 +91,28 @@ bool PhotonBeamGpuBVH::Build(const std::vector<PhotonBeam> &beams) {
         r[i] = b.radius;
         pw[3 * i] = b.powerEnd.x; pw[3 * i + 1] = b.powerEnd.y; pw[3 * i + 2] = b.powerEnd.z;
     }
-    return Check(bre_set_beams(ctx_, (int64_t)n, s.data(), e.data(), r.data(), pw.data()));
+    if (ctx_.size() == 1) return Check(bre_set_beams(ctx_[0], (int64_t)n, s.data(), e.data(), r.data(), pw.data()));
+    return Check(bre_set_beams_sharded(ctx_.data(), (int)ctx_.size(), (int64_t)n, s.data(), e.data(), r.data(),
+                                       pw.data()));
 }
 
 bool PhotonBeamGpuBVH::Gather(const SegmentRecorder &segs, float currentBeamRadius, std::vector<float> &pixelLd) {
-    if (!ctx_) return false;
+    if (!Ok()) return false;
     const int64_t npix = (int64_t)(pixelLd.size() / 3);
-    return Check(bre_gather(ctx_, segs.Size(), segs.O(), segs.P(), segs.D(), segs.TMax(), segs.Pixel(),
-                            currentBeamRadius, npix, pixelLd.data(), nullptr, nullptr));
+    if (ctx_.size() == 1)
+        return Check(bre_gather(ctx_[0], segs.Size(), segs.O(), segs.P(), segs.D(), segs.TMax(), segs.Pixel(),
+                                currentBeamRadius, npix, pixelLd.data(), nullptr, nullptr));
+    return Check(bre_gather_sharded(ctx_.data(), (int)ctx_.size(), segs.Size(), segs.O(), segs.P(), segs.D(),
+                                    segs.TMax(), segs.Pixel(), currentBeamRadius, npix, pixelLd.data(), nullptr,
+                                    nullptr));
+}
+
+bool PhotonBeamGpuBVH::Gather(const std::vector<SegmentRecorder> &recorders, float currentBeamRadius,
+                              std::vector<float> &pixelLd) {
+    merged_.Clear();
+    for (const SegmentRecorder &r : recorders) merged_.Append(r);
+    if (merged_.Size() == 0) return Ok();
+    return Gather(merged_, currentBeamRadius, pixelLd);
 }
 
 PhotonBeamParams PhotonBeamParams::FromLookup(const Lookup &ps, bool quickRender, int pixelCount) {

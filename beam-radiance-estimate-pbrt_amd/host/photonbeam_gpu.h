@@ -52,6 +52,8 @@ class SegmentRecorder {
   public:
     void Clear();
     void Record(const CameraSegment &s);
+    // Append another recorder's segments (the per-thread recorders of one pass into one batch).
+    void Append(const SegmentRecorder &other);
     int64_t Size() const { return (int64_t)tmax_.size(); }
     const float *O() const { return o_.data(); }
     const float *P() const { return p_.data(); }
@@ -64,29 +66,46 @@ class SegmentRecorder {
     std::vector<int32_t> pixel_;
 };
 
-// GPU replacement of PhotonBeamBVH for one iteration's beam set.
+// GPU replacement of PhotonBeamBVH for one iteration's beam set, on one or several GPUs.
 class PhotonBeamGpuBVH {
   public:
     explicit PhotonBeamGpuBVH(int device = 0);
+    // One libbre context per entry of `devices` (one per GPU; a repeated ordinal puts several
+    // contexts on one device): Build replicates the beam set on every device, Gather deals the
+    // coherence-sorted segment packets round-robin over them and sums their films on the host
+    // (bre_set_beams_sharded / bre_gather_sharded).  This is how a single pbrt process uses all
+    // GPUs of a node without Python or RCCL.
+    explicit PhotonBeamGpuBVH(const std::vector<int> &devices);
     ~PhotonBeamGpuBVH();
     PhotonBeamGpuBVH(const PhotonBeamGpuBVH &) = delete;
     PhotonBeamGpuBVH &operator=(const PhotonBeamGpuBVH &) = delete;
 
-    bool Ok() const { return ctx_ != nullptr; }
+    bool Ok() const { return ready_; }
+    int Devices() const { return (int)ctx_.size(); }
     // Replaces `PhotonBeamBVH photonBeamBVH(std::move(photonBeams))` (photonbeam.cpp:438).
     bool Build(const std::vector<PhotonBeam> &beams);
     // Replaces the per-segment Intersect + contribution loop (photonbeam.cpp:494-508) for all
     // recorded segments; adds into pixelLd (3 floats per pixel), like PhotonBeamPixel::Ld.
     bool Gather(const SegmentRecorder &segs, float currentBeamRadius, std::vector<float> &pixelLd);
+    // The same for every recorder of an iteration (the camera pass's per-thread recorders) in ONE
+    // batched call, so the whole iteration is sorted into coherent packets and the film crosses
+    // PCIe once per iteration.
+    bool Gather(const std::vector<SegmentRecorder> &recorders, float currentBeamRadius, std::vector<float> &pixelLd);
     bool SetOption(bre_option opt, int64_t value);
     bool Stats(bre_stats *out) const;
     const std::string &LastError() const { return err_; }
 
   private:
     bool Check(bre_status st);
-    bre_ctx *ctx_ = nullptr;
+    std::vector<bre_ctx *> ctx_;
+    bool ready_ = false;      // every context was created
+    SegmentRecorder merged_;  // concatenation buffer of Gather(recorders)
     std::string err_;
 };
+
+// The GPU ordinals of the BRE_DEVICES environment variable ("0,1,2,3"; default "0"): the
+// adapter patch's one-process multi-GPU switch.
+std::vector<int> DevicesFromEnv();
 
 // Integrator parameters with the reference's names and defaults (photonbeam.cpp:591-604).
 struct PhotonBeamParams {

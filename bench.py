@@ -105,6 +105,11 @@ def parse(argv=None):
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--segment-kind", choices=["camera", "bounce"], default="camera",
                     help="synthetic: camera primary segments or incoherent bounce segments")
+    ap.add_argument("--entry", choices=["camera", "boundary"], default="camera",
+                    help="camera (default): the in-library camera pass hands its segments to bre_gather_camera; "
+                         "boundary: the same segments in the reference's recorder order (16x16 tiles dealt to 16 "
+                         "threads, each pixel's depths in order) through bre_gather_device, the C-ABI entry the "
+                         "pbrt adapter uses")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--progress", action="store_true",
                     help="print a line per timed step to stderr (synchronises each step; long C4/C5 runs)")
@@ -307,6 +312,10 @@ def main():
             "beam_lines_staged_per_wave": st["beam_evals"] / items,
             "exact_batches_per_wave": st["ccp_wave_evals"] / items,
             "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
+            "queued_pairs_per_estimate": st["queued_pairs"] / nseg_d,
+            "contributions_per_queued_pair": st["contributions"] / max(st["queued_pairs"], 1),
+            # (lane, kept beam) prefilter tests ~ kept beams x 64 lanes; per queued pair (~7)
+            "prefilter_tests_per_queued_pair": st["useful_beam_evals"] * 64 / max(st["queued_pairs"], 1),
         })
     result.update(diag)
 
@@ -338,16 +347,21 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     nseg = max(st["n_segments"], 1)
     items = (nseg + 63) // 64 * args.split
     # what the packet algorithm must read / write per launch: every visited node line and staged
-    # beam line (64 B each) of every (packet, subtree) item, the segments (40 B in) per item, the
-    # per-subtree partial sums (12 B out), and the reduce (12 B x split in, 12 B out per segment)
-    alg = 64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + nseg * 12 * (args.split + 1)
+    # beam line (64 B each) of every (packet, subtree) item; per item the segments (40 B in) and the
+    # per-subtree partial sums (12 B out) of its 64 lanes; per queued (lane, beam) pair the exact
+    # stage's loads (the segment's four 16-B SegRec planes, the 64-B BeamRec and the 16-B power: 144
+    # B); and the reduce (12 B x split in, 12 B out per segment)
+    queued = st.get("queued_pairs", 0)
+    alg = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + 144.0 * queued
+           + nseg * 12 * (args.split + 1))
     achieved = alg / (gather_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
            "kernel": "k_gather_tile (+ k_reduce)", "launch": "iteration 0", "launch_ms": gather_ms,
-           "algorithmic_bytes_per_launch": alg,
+           "algorithmic_bytes_per_launch": alg, "queued_pairs_per_launch": queued,
            "algorithmic_model": "64 B x (node visits + beam lines staged) + 52 B x 64 per (packet, subtree) "
-                                "item + 12 B x (split + 1) per segment; counts from this run's counter pass"}
+                                "item + 144 B per queued exact-stage pair + 12 B x (split + 1) per segment; "
+                                "counts from this run's counter pass"}
     if pmc:
         out["traffic"] = pmc.get("traffic_bytes_per_launch")
         out["traffic_source"] = pmc.get("source")
@@ -356,6 +370,9 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
             out["traffic_over_algorithmic"] = out["traffic"] / alg
         if pmc.get("issue"):
             out["issue"] = pmc["issue"]
+            # the unit that binds the kernel: VALU issue, not HBM bandwidth
+            out["binding_unit"] = "valu_issue"
+            out["bound_frac"] = pmc["issue"]["valu_issue_frac"]
     if cpu and cpu.get("visit_mean"):
         # SURVEY.md §8d's reference-tree model (every segment streams its candidates from HBM):
         # kept for comparison, not a fraction of HBM peak
@@ -472,24 +489,67 @@ class SceneWorkload:
                      f"{'grid-density smoke' if preset['medium'] == 'smoke' else 'homogeneous fog'}; photons and "
                      "camera paths traced on the GPU)")
         self.last_nseg = 0
+        self.n_iter = {"c2": 16, "c5": 10}.get(self.name)
+        self._rec = {}
+        if args.entry == "boundary":  # stage every timed iteration's recorder-order segments up front
+            for k in range(max(args.steps, args.warmup)):
+                self.recorder_segments(self.iteration(k))
+            self.data += "; boundary leg: camera segments in recorder order through bre_gather_device"
 
     def radius(self, it):
         return self.bre.beam_radius_at(self.args.radius, self.args.alpha, it)
 
-    def step(self, it, ev, scratch):
+    def iteration(self, k):
+        """Step k runs the render's iteration k mod its iteration count (C2: 16, C5: 10), so a longer
+        --steps repeats the configuration's own iterations and never times smaller radii than it has."""
+        return k % self.n_iter if self.n_iter else k
+
+    def recorder_segments(self, it):
+        """Boundary leg: iteration `it`'s camera segments in the reference's recorder order, on the
+        device (untimed setup).  The camera pass of photonbeam.cpp:444-557 records per thread: 16x16
+        tiles (:345-347) dealt by ParallelFor2D to the threads (here tile t to thread t mod 16), each
+        tile's pixels row-major, each pixel's path depths in order; the recorders are concatenated in
+        thread order (the mirror's Gather(recorders))."""
+        import torch
+
+        if it in self._rec:
+            return self._rec[it]
+        g = self.g
+        g.camera_pass(self.scene, self.W, self.H, it, self.args.max_depth, True, True)
+        s = g.get_segments()
+        px = s["pixel"].astype(np.int64)
+        x, y = px % self.W, px // self.W
+        ntx = (self.W + 15) // 16
+        tile = (y // 16) * ntx + x // 16
+        key = ((((tile % 16) * (tile.max() + 1) + tile) * 256 + (y % 16) * 16 + x % 16) * 64 + s["depth"])
+        order = np.argsort(key, kind="stable")
+        dev = self.ld.device
+        rec = {k: torch.from_numpy(np.ascontiguousarray(s[k][order])).to(dev) for k in ("o", "p", "d", "tmax", "pixel")}
+        self._rec[it] = rec
+        return rec
+
+    def step(self, k, ev, scratch):
         import torch
 
         a = self.args
-        i = it % len(self.ctxs)
+        it = self.iteration(k)
+        i = k % len(self.ctxs)
         g, st = self.ctxs[i]
         ld = (self.scratch if scratch else self.films)[i]
         R = self.radius(it)
+        rec = self.recorder_segments(it) if a.entry == "boundary" else None
         with torch.cuda.stream(st):
             self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
-            n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
+            if rec is None:
+                n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
+            else:
+                n = int(rec["tmax"].shape[0])
             if ev is not None:
                 ev[0].record()
-            g.gather_camera(R, ld)  # asynchronous: the next step's passes overlap it on the other stream
+            if rec is None:
+                g.gather_camera(R, ld)  # asynchronous: the next step's passes overlap it on the other stream
+            else:  # the C-ABI boundary: caller-order device segments, sorted and gathered inside libbre
+                g.gather_device(rec["o"], rec["p"], rec["d"], rec["tmax"], rec["pixel"], R, self.W * self.H, accum=ld)
             if ev is not None:
                 ev[1].record()
         if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
@@ -546,6 +606,8 @@ class SceneWorkload:
         return {"workload": f"{self.name.upper()}: Cornell box + {med}, {a.photons / 1e6:g}M photons/iteration, "
                             f"{film}, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
                 "photons_per_iteration": a.photons, "image": [self.W, self.H], "iterations_timed": a.steps,
+                "render_iterations": self.n_iter, "entry": ("bre_gather_camera" if a.entry == "camera" else
+                                                            "bre_gather_device, recorder-order segments"),
                 "parallelism": (f"segment packets x{world} ({a.scaling} scaling), photons traced and camera pass "
                                 "on every rank, one RCCL reduce of the partial films per written image"
                                 if a.shard_mode == "packets" else
@@ -657,7 +719,7 @@ def cpu_baseline(wl, args, gather_per_step):
 
     ora = load_oracle()
     threads, cpu_note = host_threads()
-    iters = sorted({0, args.steps - 1}) if wl.name != "synthetic" else [0]
+    iters = sorted({0, wl.iteration(args.steps - 1)}) if wl.name != "synthetic" else [0]
     per_it, visit, cand = [], [], []
     for it in iters:
         beams, segs, R = wl.cpu_inputs(it)

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define BRE_ABI_VERSION 2 /* 2: triangle scene model (bre_scene.h) */
+#define BRE_ABI_VERSION 3 /* 2: triangle scene model (bre_scene.h); 3: multi-GPU entry points */
 
 typedef struct bre_ctx bre_ctx;
 
@@ -125,6 +125,8 @@ typedef struct bre_stats {
     int64_t n_camera_segments; /* segments of the last bre_camera_pass */
     double camera_ms;        /* device time of the last camera pass incl. compaction (timing only) */
     int64_t n_chunks;        /* kernel 5: chunks in the index of the last gather */
+    int64_t queued_pairs;    /* kernels 0/4, counters: (segment, beam) pairs that passed the prefilters
+                                and ran the exact stage (box test + ComputeClosestPoints) */
 } bre_stats;
 
 /* ---- context ---- */
@@ -164,7 +166,11 @@ bre_status bre_set_beams_device(bre_ctx *ctx, int64_t n, const float *d_start_xy
    synchronising call (bre_synchronize, bre_gather, bre_trace_photons, bre_camera_pass, bre_get_*,
    bre_render*).
    bre_gather takes host pointers (PCIe copies in and out, synchronous); bre_gather_device
-   takes device pointers and is asynchronous on the context's stream. */
+   takes device pointers and is asynchronous on the context's stream.  Both hand the segments to
+   the production kernel in the coherence order of bre_gather_camera (BRE_OPT_SORT_SEGMENTS, kernels
+   0 / 4) and scatter per-segment outputs back to the caller's order; under BRE_OPT_SHARD_MODE 1 with
+   a shard count > 1 they gather only this shard's packets of that order (the other entries of the
+   per-segment outputs are zeroed), exactly as bre_gather_camera does. */
 bre_status bre_gather(bre_ctx *ctx, int64_t nseg, const float *seg_o_xyz, const float *seg_p_xyz,
                       const float *seg_d_xyz, const float *seg_tmax, const int32_t *seg_pixel,
                       float beam_radius_cur, int64_t npix, float *accum_rgb, float *seg_rgb,
@@ -174,6 +180,27 @@ bre_status bre_gather_device(bre_ctx *ctx, int64_t nseg, const float *d_seg_o_xy
                              const float *d_seg_tmax, const int32_t *d_seg_pixel,
                              float beam_radius_cur, int64_t npix, float *d_accum_rgb,
                              float *d_seg_rgb, int32_t *d_seg_counts);
+
+/* ---- multi-GPU gather (SURVEY.md §8(b) `bre_gather_sharded`, §8(e)) ----
+   ctxs[0 .. n_ctx): one context per GPU (several contexts on one device are allowed: tests), each
+   driven by its own host thread for the duration of the call.  The reference renders in one
+   process over a thread pool (photonbeam.cpp:444-557); this is the same batched gather split over
+   devices with the photon map replicated.
+   bre_set_beams_sharded: bre_set_beams on every context, in parallel (the same beam set and BVH on
+   every device).
+   bre_gather_sharded: bre_gather semantics for host segments.  Context i gathers packet shard i of
+   n_ctx of the coherence-sorted segment order (BRE_OPT_SHARD_MODE 1, BRE_OPT_SHARD_BLOCK 1; each
+   context's own shard options are restored afterwards), so every device gets the same mix of cheap
+   and costly packets.  The devices' films are summed on the host in context order and added (+=)
+   into accum_rgb; per-segment outputs (each entry is gathered by exactly one context) are merged the
+   same way.  The first failing context's status is returned, its message prefixed with the context
+   index in bre_last_error(ctxs[0]). */
+bre_status bre_set_beams_sharded(bre_ctx *const *ctxs, int n_ctx, int64_t n, const float *start_xyz,
+                                 const float *end_xyz, const float *radius, const float *power_end_rgb);
+bre_status bre_gather_sharded(bre_ctx *const *ctxs, int n_ctx, int64_t nseg, const float *seg_o_xyz,
+                              const float *seg_p_xyz, const float *seg_d_xyz, const float *seg_tmax,
+                              const int32_t *seg_pixel, float beam_radius_cur, int64_t npix, float *accum_rgb,
+                              float *seg_rgb, int32_t *seg_counts);
 
 /* ---- photon pass (replaces photonbeam.cpp:362-437: emission, TracePhotonBeamRecursive and the
    merge into one beam vector, then the PhotonBeamBVH build of :438) ----

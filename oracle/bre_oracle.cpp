@@ -661,7 +661,7 @@ void ora_gather(void *hp, int64_t nseg, const float *o, const float *p, const fl
 void ora_gather_bruteforce(int64_t nb, const float *start, const float *end, const float *radius,
                            const float *powerEnd, int sqrtMode, int64_t nseg, const float *o, const float *p,
                            const float *d, const float *tmax, float R, float *seg_rgb, int64_t *seg_cand,
-                           int64_t *seg_contrib) {
+                           int64_t *seg_contrib, int nthreads) {
     std::vector<PhotonBeam> beams((size_t)nb);
     std::vector<Box> boxes((size_t)nb);
     std::vector<V3> cent((size_t)nb);
@@ -699,26 +699,35 @@ void ora_gather_bruteforce(int64_t nb, const float *start, const float *end, con
         }
         a = b;
     }
-    for (int64_t s = 0; s < nseg; ++s) {
-        Ray ray{ld3(o, s), ld3(d, s), tmax[s]};
-        V3 invDir(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-        int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-        Float acc[3] = {0, 0, 0};
-        int64_t c = 0, k = 0;
-        V3 pp = ld3(p, s);
-        for (int64_t i = 0; i < nb; ++i) {
-            if (!intersectP(gbox[i], ray, invDir, neg)) continue;
-            ++c;
-            Float rgb[3];
-            if (beamContribution(beams[i], ray.o, pp, R, rgb)) {
-                acc[0] += rgb[0]; acc[1] += rgb[1]; acc[2] += rgb[2];
-                ++k;
+    // segments are independent: nthreads workers take segments in turn (each segment's sum is
+    // still in input order, so the result does not depend on nthreads)
+    std::atomic<int64_t> next(0);
+    auto worker = [&]() {
+        for (int64_t s; (s = next.fetch_add(1)) < nseg;) {
+            Ray ray{ld3(o, s), ld3(d, s), tmax[s]};
+            V3 invDir(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+            int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+            Float acc[3] = {0, 0, 0};
+            int64_t c = 0, k = 0;
+            V3 pp = ld3(p, s);
+            for (int64_t i = 0; i < nb; ++i) {
+                if (!intersectP(gbox[i], ray, invDir, neg)) continue;
+                ++c;
+                Float rgb[3];
+                if (beamContribution(beams[i], ray.o, pp, R, rgb)) {
+                    acc[0] += rgb[0]; acc[1] += rgb[1]; acc[2] += rgb[2];
+                    ++k;
+                }
             }
+            if (seg_rgb) { seg_rgb[3 * s] = acc[0]; seg_rgb[3 * s + 1] = acc[1]; seg_rgb[3 * s + 2] = acc[2]; }
+            if (seg_cand) seg_cand[s] = c;
+            if (seg_contrib) seg_contrib[s] = k;
         }
-        if (seg_rgb) { seg_rgb[3 * s] = acc[0]; seg_rgb[3 * s + 1] = acc[1]; seg_rgb[3 * s + 2] = acc[2]; }
-        if (seg_cand) seg_cand[s] = c;
-        if (seg_contrib) seg_contrib[s] = k;
-    }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthreads; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
 }
 
 }  // extern "C"

@@ -39,7 +39,7 @@ class Oracle:
         lib.ora_bvh_max_leaf.restype = I32
         lib.ora_bvh_free.argtypes = [P]
         lib.ora_gather.argtypes = [P, I64, P, P, P, P, P, F, P, P, P, P, P, I32, I64]
-        lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P]
+        lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P, I32]
         U64 = ctypes.c_uint64
         lib.ora_trace_photons.argtypes = [P, I64, I32, I32, F, I64, P, P, P, P, P]
         lib.ora_trace_photons.restype = I64
@@ -233,7 +233,7 @@ class Oracle:
     def build(self, beams, sqrt_mode=0):
         return OracleBVH(self, beams, sqrt_mode)
 
-    def bruteforce(self, beams, segs, R, sqrt_mode=0):
+    def bruteforce(self, beams, segs, R, sqrt_mode=0, nthreads=1):
         b = {k: np.ascontiguousarray(beams[k], np.float32) for k in ("start", "end", "radius", "power")}
         s = {k: np.ascontiguousarray(segs[k], np.float32) for k in ("o", "p", "d", "tmax")}
         nb, ns = b["radius"].shape[0], s["tmax"].shape[0]
@@ -242,7 +242,7 @@ class Oracle:
         contrib = np.zeros(ns, np.int64)
         self.lib.ora_gather_bruteforce(nb, _p(b["start"]), _p(b["end"]), _p(b["radius"]), _p(b["power"]), sqrt_mode,
                                        ns, _p(s["o"]), _p(s["p"]), _p(s["d"]), _p(s["tmax"]), float(R), _p(rgb),
-                                       _p(cand), _p(contrib))
+                                       _p(cand), _p(contrib), int(nthreads))
         return {"seg_rgb": rgb, "cand": cand, "contrib": contrib}
 
 

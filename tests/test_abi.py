@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol(bre):
     lib = bre.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.bre_abi_version() == 2
+    assert lib.bre_abi_version() == 3
 
 
 def test_library_is_gfx950_code_object():

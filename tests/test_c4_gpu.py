@@ -1,0 +1,95 @@
+"""C4 at its real size on the GPU ("next round" item 1): BASELINE.json configs[3], the
+north star's scaling configuration -- the Cornell box in homogeneous fog, 2048x2048, 20M photons,
+iteration 0 (the largest radius).
+
+(a) The production gather (kernel 0, counters off, coherence sort on) of every camera segment of the
+    iteration (~9.6M estimates against ~54M beams, several tile-kernel launches under the 4 GiB
+    partial cap) is compared with the oracle on 300 sampled segments over the FULL beam set:
+    contribution counts exactly, per-segment RGB within max(1e-5, 4 u sqrt(n)).  The oracle is the
+    brute-force restatement (every beam's group box through the reference's IntersectP,
+    photonbeambvh.h:60-72 + geometry.h:1410-1436, then photonbeam.cpp:494-508); its candidate set
+    equals the SAH tree's (tests/test_oracle_crosscheck.py), and a 54M-beam SAH build would take
+    minutes on the host.
+(b) The 8 packet shards of an 8-GPU run (BRE_OPT_SHARD_MODE 1: the sorted order's 64-segment packets
+    dealt round-robin, photonbeam.cpp:344-347's tile loop split over devices) are gathered one after
+    another on this GPU; their films sum to the one-shard film (<= 1e-6 relative L2: only the float
+    order of the pixel sums differs) and their shares partition the segments.
+Reference: photonbeam.cpp:344-347, 444-557, 565-584."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W = H = 2048
+PHOTONS = 20_000_000
+NSAMPLE = 300
+WORLD = 8
+
+
+def _rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.mark.timeout(1100)
+def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
+    import torch
+
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+    it = 0
+    R = bre.beam_radius_at(0.01, 0.5, it)
+    t0 = time.perf_counter()
+    with bre.BeamGather(0) as g:  # kernel 0, counters off, sort on: the bench configuration
+        nb = g.trace_photons(scene, PHOTONS, it, 5, R)
+        n = g.camera_pass(scene, W, H, it, 5, True, True)
+        seg_rgb = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+        counts = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
+        ld1 = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
+        t1 = time.perf_counter()
+        g.gather_camera_segments(R, accum=ld1, seg_rgb=seg_rgb, counts=counts)
+        g.synchronize()
+        t2 = time.perf_counter()
+        # (b) the 8 packet shards of this iteration, one after another on this GPU
+        films = []
+        for rank in range(WORLD):
+            g.set_shard(rank, WORLD, 1, packets=True)
+            f = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
+            g.gather_camera(R, f)
+            g.synchronize()
+            films.append(f)
+        t3 = time.perf_counter()
+        g.set_shard(0, 1, 1, packets=True)
+        beams = g.get_beams()
+        segs = g.get_segments()
+    print(f"C4: {nb} beams, {n} segments; full gather {t2 - t1:.1f} s, 8 shards {t3 - t2:.1f} s "
+          f"(setup {t1 - t0:.1f} s)")
+    assert nb > 40_000_000 and n > 8_000_000
+    seg_rgb, counts = seg_rgb.cpu().numpy(), counts.cpu().numpy()
+    assert (counts[:, 0] == -1).all()
+    # the shards: partition of the segments, films summing to the one-shard film
+    assert sum(bre.shard_segments(n, r, WORLD, 1) for r in range(WORLD)) == n
+    want = ld1.cpu().numpy()
+    got = sum(f.double() for f in films).float().cpu().numpy()
+    del films
+    assert want.sum() > 0
+    assert _rel_l2(got, want) <= 1e-6
+    # the production film equals the per-segment sums added by pixel
+    acc = np.zeros((W * H, 3), np.float64)
+    np.add.at(acc, segs["pixel"], seg_rgb.astype(np.float64))
+    assert np.abs(want - acc).max() <= 1e-5 * max(float(np.abs(acc).max()), 1e-30)
+    # (a) the oracle on sampled segments against all beams
+    idx = np.random.default_rng(4000).choice(n, NSAMPLE, replace=False)
+    sample = {k: np.ascontiguousarray(segs[k][idx]) for k in ("o", "p", "d", "tmax")}
+    t4 = time.perf_counter()
+    ref = oracle.bruteforce(beams, sample, R, nthreads=16)
+    print(f"C4 oracle: {NSAMPLE} segments x {nb} beams in {time.perf_counter() - t4:.1f} s, "
+          f"{int(ref['contrib'].sum())} contributions")
+    assert ref["contrib"].sum() > 100_000
+    assert np.array_equal(counts[idx, 1], ref["contrib"]), "production contribution counts differ"
+    scale = np.maximum(np.abs(ref["seg_rgb"]).max(axis=1), 1e-30)
+    err = np.abs(seg_rgb[idx] - ref["seg_rgb"]).max(axis=1) / scale
+    tol = np.maximum(1e-5, 4 * 2.0 ** -24 * np.sqrt(ref["contrib"].astype(np.float64)))
+    worst = int(np.argmax(err / tol))
+    assert (err <= tol).all(), (float(err[worst]), float(tol[worst]), int(ref["contrib"][worst]))
