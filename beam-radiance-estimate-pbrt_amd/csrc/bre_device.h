@@ -208,7 +208,8 @@ struct SegSort {
     size_t tmp_bytes;
     float *o2, *p2, *d2, *t2;  // sorted copies
     int32_t *pix2;
-    int key_mode;  // 0: Morton of (origin, octahedral direction); 1: Morton of (origin, end point)
+    int key_mode;  // 0: Morton of (origin, octahedral direction); 1: Morton of (origin, end point);
+                   // 2 / 3: the segment's line (dominant-axis class + slopes + plane crossing [+ midpoint])
 };
 size_t seg_sort_temp_bytes(int64_t n);
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);

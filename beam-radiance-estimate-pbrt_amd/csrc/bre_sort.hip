@@ -160,6 +160,82 @@ __global__ __launch_bounds__(kBlock) void k_seg_keys_op(int64_t n, const float *
     vals[i] = (int32_t)i;
 }
 
+// Line keys (modes 2 / 3): the packet kernels' bundle reject measures how far the packet's segments
+// lie from ONE line, so segments on nearly the same infinite line belong together wherever they sit
+// along it.  The key is the segment's line: a class of 3 bits for the dominant axis a of its
+// direction and that component's sign, then Morton bits of the two slopes dir_b / |dir_a|,
+// dir_c / |dir_a| (in [-1, 1]) and of the point where the line crosses the plane x_a = centre_a of
+// the segments' box (the other two coordinates, in the box grown by its extent on both sides).
+// Mode 2 interleaves these 4 coordinates with 14 bits each; mode 3 adds the segment midpoint's
+// coordinate along the dominant axis as a fifth, with 11 bits each.
+__device__ __forceinline__ unsigned int quant_bits(float x, int bits) {  // x in [0, 1]
+    const float m = (float)((1u << bits) - 1u);
+    return (unsigned int)(fminf(fmaxf(x, 0.f), 1.f) * m);
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_keys_line(int64_t n, const float *__restrict__ o,
+                                                          const float *__restrict__ p, const float *__restrict__ d,
+                                                          const unsigned int *__restrict__ b, int five,
+                                                          unsigned long long *__restrict__ keys,
+                                                          int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float lo[3] = {ord2f(b[0]), ord2f(b[1]), ord2f(b[2])};
+    const float hi[3] = {ord2f(b[3]), ord2f(b[4]), ord2f(b[5])};
+    const float O[3] = {o[3 * i], o[3 * i + 1], o[3 * i + 2]};
+    const float P[3] = {p[3 * i], p[3 * i + 1], p[3 * i + 2]};
+    float v[3] = {P[0] - O[0], P[1] - O[1], P[2] - O[2]};
+    if (!(fabsf(v[0]) + fabsf(v[1]) + fabsf(v[2]) > 0.f)) {  // zero-length segment: its ray direction
+        v[0] = d[3 * i];
+        v[1] = d[3 * i + 1];
+        v[2] = d[3 * i + 2];
+    }
+    int a = 0;
+    if (fabsf(v[1]) > fabsf(v[a])) a = 1;
+    if (fabsf(v[2]) > fabsf(v[a])) a = 2;
+    const int b1 = a == 0 ? 1 : 0, b2 = a == 2 ? 1 : 2;
+    const float va = v[a];
+    const unsigned int cls = (unsigned int)(2 * a + (va < 0.f ? 1 : 0));
+    const float ia = va != 0.f && isfinite(va) ? 1.f / fabsf(va) : 0.f;
+    float q[5];
+    q[0] = 0.5f * (v[b1] * ia) + 0.5f;  // slopes in [-1, 1] -> [0, 1]
+    q[1] = 0.5f * (v[b2] * ia) + 0.5f;
+    const float ca = 0.5f * (lo[a] + hi[a]);
+    const float t = va != 0.f ? (ca - O[a]) / va : 0.f;
+    const int bb[2] = {b1, b2};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int c = bb[k];
+        const float ext = hi[c] - lo[c];
+        const float x = O[c] + t * v[c];
+        q[2 + k] = ext > 0.f ? (x - (lo[c] - ext)) / (3.f * ext) : 0.f;
+    }
+    {
+        const float ext = hi[a] - lo[a];
+        q[4] = ext > 0.f ? (0.5f * (O[a] + P[a]) - lo[a]) / ext : 0.f;
+    }
+    unsigned long long key = cls;
+    if (five) {
+        unsigned int u[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) u[k] = quant_bits(isfinite(q[k]) ? q[k] : 0.f, 11);
+#pragma unroll
+        for (int bit = 10; bit >= 0; --bit)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) key = (key << 1) | ((u[k] >> bit) & 1u);
+    } else {
+        unsigned int u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = quant_bits(isfinite(q[k]) ? q[k] : 0.f, 14);
+#pragma unroll
+        for (int bit = 13; bit >= 0; --bit)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) key = (key << 1) | ((u[k] >> bit) & 1u);
+    }
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
 __global__ __launch_bounds__(kBlock) void k_seg_permute(int64_t n, const int32_t *__restrict__ order,
                                                         const float *__restrict__ o, const float *__restrict__ p,
                                                         const float *__restrict__ d, const float *__restrict__ t,
@@ -222,7 +298,7 @@ hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chu
 size_t seg_sort_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 60);
+                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 64);  // the widest key any mode sorts
     return bytes;
 }
 
@@ -231,10 +307,17 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     hipLaunchKernelGGL(k_sort_init, dim3(1), dim3(64), 0, st, s.bounds);
     const unsigned bgrid = grid_of(s.n) < 1024u ? grid_of(s.n) : 1024u;  // grid-stride bounds
     hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
+    int key_bits = 50;
     if (s.key_mode == 1) {
         hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
         hipLaunchKernelGGL(k_seg_keys_op, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.bounds, s.keys,
                            s.vals);
+        key_bits = 60;
+    } else if (s.key_mode == 2 || s.key_mode == 3) {
+        hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
+        hipLaunchKernelGGL(k_seg_keys_line, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.d, s.bounds,
+                           s.key_mode == 3 ? 1 : 0, s.keys, s.vals);
+        key_bits = s.key_mode == 3 ? 58 : 59;
     } else {
         hipLaunchKernelGGL(k_seg_keys, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.d, s.bounds, s.keys,
                            s.vals);
@@ -242,7 +325,7 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.tmp_bytes;
-    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, s.key_mode == 1 ? 60 : 50, st);
+    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
                        s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);
