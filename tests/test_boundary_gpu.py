@@ -152,7 +152,7 @@ def test_gather_sharded_equals_one_context(bre, synth, oracle, nctx):
     ctxs = [bre.BeamGather(0) for _ in range(nctx)]
     try:
         bre.set_beams_sharded(ctxs, beams["start"], beams["end"], beams["radius"], beams["power"])
-        acc = np.ones((npix, 3), np.float32)  # += semantics
+        acc = one_acc.copy()  # += semantics: the result is twice the one-context film
         out = bre.gather_sharded(ctxs, segs["o"], segs["p"], segs["d"], segs["tmax"], segs["pixel"], R=R,
                                  npix=npix, accum=acc, counts=True)
     finally:
@@ -161,8 +161,8 @@ def test_gather_sharded_equals_one_context(bre, synth, oracle, nctx):
     assert np.array_equal(out["counts"], one["counts"])
     assert np.array_equal(out["counts"][:, 1], ref["contrib"])
     assert np.array_equal(out["seg_rgb"], one["seg_rgb"])
-    assert _rel_l2(acc - 1.0, one_acc) <= 1e-6
-    assert _rel_l2(acc - 1.0, ref["accum"]) <= 1e-6
+    assert _rel_l2(acc, 2 * one_acc) <= 1e-6
+    assert _rel_l2(acc, 2 * ref["accum"]) <= 1e-6
 
 
 def test_gather_sharded_rejects_repeated_context(bre, synth):
