@@ -358,4 +358,79 @@ void ora_distribution1d(const float *func, int32_t nf, int64_t m, const float *u
     for (int i = 0; i < nf; ++i) dpdf[i] = dist.DiscretePDF(i);
 }
 
+// Distribution1D::SampleContinuous for m values of u: x, pdf, offset (Distribution1D.Continuous,
+// sampling.cpp:282-303)
+void ora_distribution1d_continuous(const float *func, int32_t nf, int64_t m, const float *u, float *x, float *pdf,
+                                   int32_t *off) {
+    const orp::Distribution1D dist(func, nf);
+    for (int64_t i = 0; i < m; ++i) {
+        int o = 0;
+        x[i] = dist.SampleContinuous(u[i], &pdf[i], &o);
+        off[i] = o;
+    }
+}
+
+// Triangle.Reintersect (src/tests/shapes.cpp:154-208) on the oracle's pbrt primitives, with the
+// test's own random streams: triangle i's vertices, sample point and ray origin come from RNG(i)
+// through pExp (shapes.cpp:18-21: 10^Lerp(u, -8, 8), std::pow in double); a ray from the origin to
+// Triangle::Sample's point is intersected (Triangle::Intersect, with its pError), and
+// rays_per_tri rays leaving the hit -- SpawnRay along UniformSampleSphere directions and SpawnRayTo
+// random pExp points (interaction.h:64-72, OffsetRayOrigin geometry.h:1438-1458, ShadowEpsilon
+// pbrt.h:178) -- must not hit the triangle again.  Returns the re-intersections (the reference
+// expects none); *tested: spawned rays checked, *used: triangles whose first ray hit.
+int64_t ora_tri_reintersect(int32_t n_tris, int32_t rays_per_tri, int64_t *tested, int32_t *used) {
+    using namespace orp;
+    int64_t bad = 0, nt = 0;
+    int32_t nu = 0;
+    for (int i = 0; i < n_tris; ++i) {
+        RNG rng((uint64_t)i);
+        const auto pExp = [&]() {
+            const Float logu = Lerp(rng.UniformFloat(), -8.f, 8.f);
+            return (Float)std::pow(10, logu);
+        };
+        V3 v[3];
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) v[j][k] = pExp();
+        if (Cross(v[1] - v[0], v[2] - v[0]).LengthSquared() < 1e-20f) continue;  // GetRandomTriangle
+        bre_scene bs;
+        std::memset(&bs, 0, sizeof(bs));
+        bs.n_triangles = 1;
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) bs.triangles[0].p[j][k] = v[j][k];
+        const Scene sc = make_scene(&bs);
+        const Tri &T = sc.tris[0];
+        Float u0 = rng.UniformFloat();
+        Float u1 = rng.UniformFloat();
+        const ShapeSample pTri = SampleTri(T, u0, u1);
+        V3 o;
+        for (int j = 0; j < 3; ++j) o[j] = pExp();
+        Ray r{o, pTri.p - o, Infinity};
+        Float tHit;
+        Isect isect;
+        if (!IntersectTri(T, r, &tHit, &isect)) continue;
+        ++nu;
+        for (int j = 0; j < rays_per_tri; ++j) {
+            u0 = rng.UniformFloat();
+            u1 = rng.UniformFloat();
+            // UniformSampleSphere (sampling.cpp:98-103)
+            const Float z = 1 - 2 * u0;
+            const Float rr = std::sqrt(std::max((Float)0, (Float)1 - z * z));
+            const Float phi = 2 * Pi * u1;
+            const V3 w(rr * std::cos(phi), rr * std::sin(phi), z);
+            Ray out{OffsetRayOrigin(isect.p, isect.pError, isect.n, w), w, Infinity};  // SpawnRay(w)
+            Isect tmp;
+            bad += IntersectTri(T, out, &tHit, &tmp) ? 1 : 0;
+            V3 p2;
+            for (int k = 0; k < 3; ++k) p2[k] = pExp();
+            // SpawnRayTo(p2): origin offset toward p2, d = p2 - p, tMax = 1 - ShadowEpsilon
+            Ray to{OffsetRayOrigin(isect.p, isect.pError, isect.n, p2 - isect.p), p2 - isect.p, 1 - 0.0001f};
+            bad += IntersectTri(T, to, &tHit, &tmp) ? 1 : 0;
+            nt += 2;
+        }
+    }
+    if (tested) *tested = nt;
+    if (used) *used = nu;
+    return bad;
+}
+
 }  // extern "C"

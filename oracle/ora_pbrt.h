@@ -281,6 +281,26 @@ struct Distribution1D {
         return offset;
     }
     Float DiscretePDF(int index) const { return func[index] / (funcInt * (Float)Count()); }
+    // SampleContinuous (sampling.h:71-89): the same FindInterval, then the offset along the segment
+    Float SampleContinuous(Float u, Float *pdf, int *off = nullptr) const {
+        const int size = (int)cdf.size();
+        int first = 0, len = size;
+        while (len > 0) {
+            int half = len >> 1, middle = first + half;
+            if (cdf[middle] <= u) {
+                first = middle + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        const int offset = std::min(std::max(first - 1, 0), size - 2);
+        if (off) *off = offset;
+        Float du = u - cdf[offset];
+        if ((cdf[offset + 1] - cdf[offset]) > 0) du /= (cdf[offset + 1] - cdf[offset]);
+        if (pdf) *pdf = (funcInt > 0) ? func[offset] / funcInt : 0;
+        return (offset + du) / Count();
+    }
 };
 
 struct Scene {

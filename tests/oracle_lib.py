@@ -64,6 +64,9 @@ class Oracle:
         lib.ora_tri_hits.argtypes = [P, I64, P, P, P]
         lib.ora_tri_sample.argtypes = [P, I32, I64, P, P, P, P]
         lib.ora_distribution1d.argtypes = [P, I32, I64, P, P, P, P, P]
+        lib.ora_distribution1d_continuous.argtypes = [P, I32, I64, P, P, P, P]
+        lib.ora_tri_reintersect.argtypes = [I32, I32, P, P]
+        lib.ora_tri_reintersect.restype = I64
 
     # -- primitives --
     def set_libm(self, on: bool):
@@ -177,6 +180,21 @@ class Oracle:
         dpdf = np.zeros(func.shape[0], np.float32)
         self.lib.ora_distribution1d(_p(func), func.shape[0], m, _p(u), _p(idx), _p(pdf), _p(urem), _p(dpdf))
         return idx, pdf, urem, dpdf
+
+    def distribution1d_continuous(self, func, u):
+        """Distribution1D(func).SampleContinuous(u) -> (x, pdf, offset)."""
+        func, u = np.ascontiguousarray(func, np.float32), np.ascontiguousarray(u, np.float32)
+        m = u.shape[0]
+        x, pdf, off = np.zeros(m, np.float32), np.zeros(m, np.float32), np.zeros(m, np.int32)
+        self.lib.ora_distribution1d_continuous(_p(func), func.shape[0], m, _p(u), _p(x), _p(pdf), _p(off))
+        return x, pdf, off
+
+    def tri_reintersect(self, n_tris=1000, rays_per_tri=10000):
+        """Triangle.Reintersect (shapes.cpp:154-208): (re-intersections, rays tested, triangles used)."""
+        tested, used = ctypes.c_int64(0), ctypes.c_int32(0)
+        bad = int(self.lib.ora_tri_reintersect(int(n_tris), int(rays_per_tri), ctypes.byref(tested),
+                                               ctypes.byref(used)))
+        return bad, tested.value, used.value
 
     def grid_density(self, scene, p):
         p = np.ascontiguousarray(p, np.float32)

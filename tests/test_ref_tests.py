@@ -8,7 +8,12 @@ oracle's photon and camera passes, tests/test_photon_gpu.py, tests/test_camera_g
 * Triangle.Sampling (shapes.cpp:205-272): the solid angle of random triangles from
   Triangle::Sample agrees with uniform-sphere hit counting within 10%;
 * Distribution1D.Discrete (src/tests/sampling.cpp:231-280): SampleDiscrete on {0, 1, 0, 3} with the
-  reference's exact values (the light-power choice of the photon pass).
+  reference's exact values (the light-power choice of the photon pass);
+* Triangle.Reintersect (shapes.cpp:154-208): rays spawned from a triangle hit (SpawnRay /
+  SpawnRayTo, the pError offset of OffsetRayOrigin that every photon and camera bounce uses) never
+  hit the triangle again -- restated in C on the oracle with the test's own RNG(i) streams and counts
+  (1000 triangles x 10,000 x 2 rays);
+* Distribution1D.Continuous (sampling.cpp:282-303): SampleContinuous on {1, 1, 2, 4, 8}.
 Restated with numpy's RNG in place of pbrt's (the properties, not the random streams, are tested);
 the sphere mesh is 8 x 9 instead of 16 x 16 (bre_scene holds 128 triangles), the ray count 20,000
 instead of 100,000.
@@ -153,3 +158,21 @@ def test_distribution1d_discrete(oracle):  # sampling.cpp:231-280
     got, _, _, _ = oracle.distribution1d(func, np.array(sweep, np.float32))
     k = int(np.argmax(got == 3))
     assert got[k] == 3 and (got[:k] == 1).all() and (got[k:] == 3).all() and sweep[k] < hi
+
+
+def test_triangle_reintersect(oracle):  # shapes.cpp:154-208, the reference's own counts
+    bad, tested, used = oracle.tri_reintersect(1000, 10000)
+    assert used > 900  # "we should almost always find an intersection"
+    assert tested == used * 10000 * 2
+    assert bad == 0, f"{bad} of {tested} spawned rays re-intersected their triangle"
+
+
+def test_distribution1d_continuous(oracle):  # sampling.cpp:282-303
+    func = np.array([1, 1, 2, 4, 8], np.float32)
+    x, pdf, off = oracle.distribution1d_continuous(func, np.array([0.0, 0.5, 0.75, 1.0], np.float32))
+    assert x[0] == 0.0 and off[0] == 0
+    assert pdf[0] == pytest.approx(5 * 1.0 / 16.0, rel=4 * 2.0 ** -23)  # Count() * 1 / 16
+    assert x[1] == pytest.approx(0.8, rel=4 * 2.0 ** -23)  # the boundary between the 4 and the 8 segments
+    assert x[2] == pytest.approx(0.9, rel=4 * 2.0 ** -23)  # middle of the 8 segment
+    assert pdf[2] == pytest.approx(5 * 8.0 / 16.0, rel=4 * 2.0 ** -23) and off[2] == 4
+    assert x[3] == pytest.approx(1.0, rel=4 * 2.0 ** -23)
