@@ -70,6 +70,7 @@ struct bre_ctx {
     int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
+    int beam_key = 0;        // internal: beam sort key of the tree build (BuildBuffers::beam_key)
     int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -162,6 +163,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.n = n;
     b.sqrt_mode = c->sqrt_mode;
     b.leaf_size = c->leaf_size;
+    b.beam_key = c->beam_key;
     b.box = c->box.as<float>();
     b.cent = c->cent.as<float>();
     b.cbounds = c->cbounds.as<unsigned int>();
@@ -623,6 +625,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
+    case 110: c->beam_key = value == 1 ? 1 : 0; return BRE_OK;  // internal: beam sort key (study)
     case 109:  // internal: tile kernel partial-sum bytes per launch, in MiB (tests force several launches)
         if (value < 1 || value > ((int64_t)1 << 20)) return fail(c, BRE_ERR_INVALID_ARG, "partial cap must be in 1..2^20 MiB");
         c->partial_cap = value << 20;

@@ -163,6 +163,45 @@ __global__ __launch_bounds__(kBlock) void k_morton(const float *__restrict__ box
     vals[i] = (int32_t)i;
 }
 
+// Experimental beam key (BuildBuffers::beam_key 1): a 60-bit Morton key of the beam's start AND end
+// point (10 bits each, in the centroid box, clamped), so a leaf tile holds beams with both ends close
+// (a coherent line bundle) instead of beams with close centroids and any direction.  Speed study only:
+// the equal-centroid group boxes of k_pack are only found inside equal-key runs.
+__device__ __forceinline__ unsigned int q10(float x, float lo, float ext) {
+    float u = ext > 0.0f ? (x - lo) / ext : 0.0f;
+    u = fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
+    return (unsigned int)u;
+}
+__global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ box, const float *__restrict__ cent,
+                                                      const float *__restrict__ start, const float *__restrict__ end,
+                                                      const unsigned int *__restrict__ cbounds, int64_t n,
+                                                      unsigned long long *__restrict__ keys,
+                                                      int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float b[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = box[6 * i + k];
+    const float c[3] = {cent[3 * i], cent[3 * i + 1], cent[3 * i + 2]};
+    unsigned long long key = ~0ull;
+    if (finite6(b) && isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2])) {
+        unsigned int q[6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float lo = ord2f(cbounds[k]), hi = ord2f(cbounds[3 + k]);
+            q[k] = q10(start[3 * i + k], lo, hi - lo);
+            q[3 + k] = q10(end[3 * i + k], lo, hi - lo);
+        }
+        key = 0ull;
+#pragma unroll
+        for (int bit = 9; bit >= 0; --bit)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+    }
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
 __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start, const float *__restrict__ end,
                                                  const float *__restrict__ radius, const float *__restrict__ power,
                                                  const float *__restrict__ box, const float *__restrict__ cent,
@@ -363,8 +402,12 @@ hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
 
 hipError_t launch_morton(const BuildBuffers &b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_morton, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.cbounds, b.n, b.keys,
-                       b.vals);
+    if (b.beam_key == 1 && b.start && b.end)
+        hipLaunchKernelGGL(k_morton_se, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.start, b.end,
+                           b.cbounds, b.n, b.keys, b.vals);
+    else
+        hipLaunchKernelGGL(k_morton, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.cbounds, b.n, b.keys,
+                           b.vals);
     return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ struct BuildBuffers {
     int64_t n;
     int sqrt_mode;
     int leaf_size;
+    int beam_key = 0;  // 0: Morton of the box centroid; 1 (study): Morton of (start, end)
     // scratch
     float *box;        // 6n (input order)
     float *cent;       // 3n (input order)

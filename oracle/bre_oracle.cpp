@@ -661,7 +661,7 @@ void ora_gather(void *hp, int64_t nseg, const float *o, const float *p, const fl
 void ora_gather_bruteforce(int64_t nb, const float *start, const float *end, const float *radius,
                            const float *powerEnd, int sqrtMode, int64_t nseg, const float *o, const float *p,
                            const float *d, const float *tmax, float R, float *seg_rgb, int64_t *seg_cand,
-                           int64_t *seg_contrib, int nthreads) {
+                           int64_t *seg_contrib, int nthreads, double *seg_rgb_exact) {
     std::vector<PhotonBeam> beams((size_t)nb);
     std::vector<Box> boxes((size_t)nb);
     std::vector<V3> cent((size_t)nb);
@@ -708,6 +708,7 @@ void ora_gather_bruteforce(int64_t nb, const float *start, const float *end, con
             V3 invDir(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
             int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
             Float acc[3] = {0, 0, 0};
+            double dacc[3] = {0, 0, 0};  // the same float terms summed in double (test reference)
             int64_t c = 0, k = 0;
             V3 pp = ld3(p, s);
             for (int64_t i = 0; i < nb; ++i) {
@@ -716,10 +717,13 @@ void ora_gather_bruteforce(int64_t nb, const float *start, const float *end, con
                 Float rgb[3];
                 if (beamContribution(beams[i], ray.o, pp, R, rgb)) {
                     acc[0] += rgb[0]; acc[1] += rgb[1]; acc[2] += rgb[2];
+                    dacc[0] += rgb[0]; dacc[1] += rgb[1]; dacc[2] += rgb[2];
                     ++k;
                 }
             }
             if (seg_rgb) { seg_rgb[3 * s] = acc[0]; seg_rgb[3 * s + 1] = acc[1]; seg_rgb[3 * s + 2] = acc[2]; }
+            if (seg_rgb_exact)
+                for (int q = 0; q < 3; ++q) seg_rgb_exact[3 * s + q] = dacc[q];
             if (seg_cand) seg_cand[s] = c;
             if (seg_contrib) seg_contrib[s] = k;
         }

@@ -39,7 +39,7 @@ class Oracle:
         lib.ora_bvh_max_leaf.restype = I32
         lib.ora_bvh_free.argtypes = [P]
         lib.ora_gather.argtypes = [P, I64, P, P, P, P, P, F, P, P, P, P, P, I32, I64]
-        lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P, I32]
+        lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P, I32, P]
         U64 = ctypes.c_uint64
         lib.ora_trace_photons.argtypes = [P, I64, I32, I32, F, I64, P, P, P, P, P]
         lib.ora_trace_photons.restype = I64
@@ -256,12 +256,14 @@ class Oracle:
         s = {k: np.ascontiguousarray(segs[k], np.float32) for k in ("o", "p", "d", "tmax")}
         nb, ns = b["radius"].shape[0], s["tmax"].shape[0]
         rgb = np.zeros((ns, 3), np.float32)
+        rgb_exact = np.zeros((ns, 3), np.float64)
         cand = np.zeros(ns, np.int64)
         contrib = np.zeros(ns, np.int64)
         self.lib.ora_gather_bruteforce(nb, _p(b["start"]), _p(b["end"]), _p(b["radius"]), _p(b["power"]), sqrt_mode,
                                        ns, _p(s["o"]), _p(s["p"]), _p(s["d"]), _p(s["tmax"]), float(R), _p(rgb),
-                                       _p(cand), _p(contrib), int(nthreads))
-        return {"seg_rgb": rgb, "cand": cand, "contrib": contrib}
+                                       _p(cand), _p(contrib), int(nthreads), _p(rgb_exact))
+        # seg_rgb: the reference's float sum in beam order; seg_rgb_exact: the same terms in double
+        return {"seg_rgb": rgb, "seg_rgb_exact": rgb_exact, "cand": cand, "contrib": contrib}
 
 
 class OracleBVH:

@@ -5,7 +5,8 @@ iteration 0 (the largest radius).
 (a) The production gather (kernel 0, counters off, coherence sort on) of every camera segment of the
     iteration (~9.6M estimates against ~54M beams, several tile-kernel launches under the 4 GiB
     partial cap) is compared with the oracle on 300 sampled segments over the FULL beam set:
-    contribution counts exactly, per-segment RGB within max(1e-5, 4 u sqrt(n)).  The oracle is the
+    contribution counts exactly, per-segment RGB within max(1e-5, 4 u sqrt(n)) of the exact (double)
+    sum of the oracle's float terms (the reference's own float sum is reported beside it).  The oracle is the
     brute-force restatement (every beam's group box through the reference's IntersectP,
     photonbeambvh.h:60-72 + geometry.h:1410-1436, then photonbeam.cpp:494-508); its candidate set
     equals the SAH tree's (tests/test_oracle_crosscheck.py), and a 54M-beam SAH build would take
@@ -88,8 +89,16 @@ def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
           f"{int(ref['contrib'].sum())} contributions")
     assert ref["contrib"].sum() > 100_000
     assert np.array_equal(counts[idx, 1], ref["contrib"]), "production contribution counts differ"
-    scale = np.maximum(np.abs(ref["seg_rgb"]).max(axis=1), 1e-30)
-    err = np.abs(seg_rgb[idx] - ref["seg_rgb"]).max(axis=1) / scale
+    # C4 segments have up to ~2.5M contributions: the reference's own float32 sum in beam order drifts
+    # beyond the statistical 4 u sqrt(n) bound at that length (measured 4.1e-4 relative, 4.3 u sqrt(n)),
+    # so the GPU's per-segment sums are held to the exact (double) sum of the same float terms, and the
+    # float-order sum is reported beside them
+    exact = ref["seg_rgb_exact"]
+    scale = np.maximum(np.abs(exact).max(axis=1), 1e-30)
+    err = np.abs(seg_rgb[idx].astype(np.float64) - exact).max(axis=1) / scale
     tol = np.maximum(1e-5, 4 * 2.0 ** -24 * np.sqrt(ref["contrib"].astype(np.float64)))
     worst = int(np.argmax(err / tol))
+    ref_err = np.abs(ref["seg_rgb"].astype(np.float64) - exact).max(axis=1) / scale
+    print(f"C4 per-segment error vs the exact sum: GPU max {err.max():.2e}, reference-order float sum max "
+          f"{ref_err.max():.2e}")
     assert (err <= tol).all(), (float(err[worst]), float(tol[worst]), int(ref["contrib"][worst]))
