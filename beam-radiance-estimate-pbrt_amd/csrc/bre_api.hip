@@ -94,6 +94,10 @@ struct bre_ctx {
     DevMem counters_buf, roots, partial, pcnt, segrec;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
+    // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
+    DevMem sc_tris, sc_nodes, sc_prims, sc_light_tri, sc_light_func, sc_light_cdf;
+    uint64_t sc_hash = 0;  // hash of the uploaded triangles (0: none)
+    DevScene sc_head;      // geometry fields of the uploaded scene
     // camera pass
     DevMem cam_dev, cam_perms, cs_o, cs_p, cs_d, cs_t, cs_pix, cs_valid, cam_offs, cam_tmp, cam_flags;
     DevMem seg_o, seg_p, seg_d, seg_t, seg_pix, seg_depth;
@@ -548,7 +552,8 @@ void bre_destroy(bre_ctx *c) {
                      &c->ch_offsets, &c->ch_range, &c->ch_scan_tmp, &c->ch_box, &c->ch_cent, &c->ch_slo, &c->ch_shi,
                      &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
-                     &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index};
+                     &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index,
+                     &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
@@ -731,15 +736,36 @@ static bre_status check_medium(bre_ctx *c, const bre_scene *scene, const char *f
 // Triangle count in range and at least one area light (the passes need scene.lights non-empty)
 static bre_status check_scene(bre_ctx *c, const bre_scene *scene, const char *fn) {
     if (!scene) return fail(c, BRE_ERR_INVALID_ARG, "%s: null scene", fn);
-    if (scene->n_triangles < 1 || scene->n_triangles > BRE_MAX_TRIANGLES)
-        return fail(c, BRE_ERR_INVALID_ARG, "%s: triangle count must be in 1..%d", fn, BRE_MAX_TRIANGLES);
-    int lights = 0;
-    for (int i = 0; i < scene->n_triangles; ++i) lights += scene->triangles[i].emit != 0;
+    const int cap = scene->triangles_ext ? BRE_MAX_SCENE_TRIANGLES : BRE_MAX_TRIANGLES;
+    if (scene->n_triangles < 1 || scene->n_triangles > cap)
+        return fail(c, BRE_ERR_INVALID_ARG, "%s: triangle count must be in 1..%d (%s)", fn, cap,
+                    scene->triangles_ext ? "triangles_ext" : "inline triangles; use triangles_ext for more");
+    const bre_triangle *tri = scene_triangles(scene);
+    int64_t lights = 0;
+    for (int i = 0; i < scene->n_triangles; ++i) lights += tri[i].emit != 0;
     if (lights == 0) return fail(c, BRE_ERR_INVALID_ARG, "%s: the scene has no area light", fn);
     return BRE_OK;
 }
 
-// DevScene (+ the density grid of a GridDensityMedium) into ph_scene on the context's stream
+// 64-bit hash of the scene's triangles (the geometry cache key of upload_scene)
+static uint64_t hash_triangles(const bre_scene *s) {
+    const bre_triangle *tri = scene_triangles(s);
+    const size_t bytes = (size_t)s->n_triangles * sizeof(bre_triangle);
+    const unsigned char *p = reinterpret_cast<const unsigned char *>(tri);
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)s->n_triangles;
+    size_t i = 0;
+    for (; i + 8 <= bytes; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    for (; i < bytes; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h | 1ull;  // never 0 (= no scene)
+}
+
+// DevScene (+ the density grid of a GridDensityMedium) into ph_scene on the context's stream.  The
+// geometry (triangles, BVHAccel, lights) is rebuilt and uploaded only when the triangles change.
 static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
     const float *dd = nullptr;
     if (scene->has_medium == BRE_MEDIUM_GRID) {
@@ -749,10 +775,38 @@ static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
                                  c->stream));
         dd = c->grid_dens.as<float>();
     }
-    DevScene hs;
-    prepare_scene(scene, &hs, dd);
+    const uint64_t h = hash_triangles(scene);
+    if (h != c->sc_hash) {
+        HostScene hs;
+        prepare_geometry(scene, &hs);
+        if (hs.depth > kSceneStack)
+            return fail(c, BRE_ERR_INVALID_ARG, "scene BVH depth %d exceeds the %d-entry traversal stack (as in "
+                        "BVHAccel::Intersect)", hs.depth, kSceneStack);
+        const auto up = [&](DevMem &m, const void *src, size_t bytes) -> hipError_t {
+            hipError_t e = m.ensure(bytes > 0 ? bytes : 4);
+            if (e != hipSuccess || bytes == 0) return e;
+            return hipMemcpyAsync(m.ptr, src, bytes, hipMemcpyHostToDevice, c->stream);
+        };
+        HIPCHK(c, up(c->sc_tris, hs.tris.data(), hs.tris.size() * sizeof(PTri)));
+        HIPCHK(c, up(c->sc_nodes, hs.nodes.data(), hs.nodes.size() * sizeof(SceneNode)));
+        HIPCHK(c, up(c->sc_prims, hs.prims.data(), hs.prims.size() * sizeof(int32_t)));
+        HIPCHK(c, up(c->sc_light_tri, hs.light_tri.data(), hs.light_tri.size() * sizeof(int32_t)));
+        HIPCHK(c, up(c->sc_light_func, hs.light_func.data(), hs.light_func.size() * sizeof(float)));
+        HIPCHK(c, up(c->sc_light_cdf, hs.light_cdf.data(), hs.light_cdf.size() * sizeof(float)));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // the host vectors go out of scope
+        c->sc_head = hs.head;
+        c->sc_head.t = c->sc_tris.as<PTri>();
+        c->sc_head.nodes = c->sc_nodes.as<SceneNode>();
+        c->sc_head.prims = c->sc_prims.as<int32_t>();
+        c->sc_head.light_tri = c->sc_light_tri.as<int32_t>();
+        c->sc_head.light_func = c->sc_light_func.as<float>();
+        c->sc_head.light_cdf = c->sc_light_cdf.as<float>();
+        c->sc_hash = h;
+    }
+    DevScene ds = c->sc_head;
+    prepare_medium(scene, &ds, dd);
     HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
-    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &hs, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &ds, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
     // the host copies are read by the DMA before the call returns
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BRE_OK;

@@ -18,6 +18,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <vector>
 
 #include "bre_device.h"
 #include "bre_trace.h"
@@ -31,9 +32,8 @@ float grid_max_density(const bre_scene *s) {
     return mx;
 }
 
-void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
-    DevScene d{};
-    d.n_tris = s->n_triangles;
+void prepare_medium(const bre_scene *s, DevScene *dp, const float *d_density) {
+    DevScene &d = *dp;
     d.medium = s->has_medium == BRE_MEDIUM_GRID ? BRE_MEDIUM_GRID : (s->has_medium ? BRE_MEDIUM_HOMOGENEOUS : 0);
     if (d.medium == BRE_MEDIUM_GRID) {
         // GridDensityMedium ctor (grid.h:58-77): sigma_t = (sigma_a + sigma_s)[0]; invMaxDensity
@@ -46,10 +46,18 @@ void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
     for (int c = 0; c < 3; ++c)
         d.sigma_t[c] = s->sigma_a[c] + s->sigma_s[c];  // HomogeneousMedium ctor: sigma_a + sigma_s
     d.g = s->g;
-    int nl = 0;
+}
+
+void prepare_geometry(const bre_scene *s, HostScene *out) {
+    DevScene &d = out->head;
+    d.n_tris = s->n_triangles;
+    const bre_triangle *tri = scene_triangles(s);
+    out->tris.resize((size_t)s->n_triangles);
+    out->light_tri.clear();
+    out->light_func.clear();
     for (int i = 0; i < s->n_triangles; ++i) {
-        const bre_triangle &t = s->triangles[i];
-        PTri &T = d.t[i];
+        const bre_triangle &t = tri[i];
+        PTri &T = out->tris[(size_t)i];
         T.p0 = mk(t.p[0][0], t.p[0][1], t.p[0][2]);
         T.p1 = mk(t.p[1][0], t.p[1][1], t.p[1][2]);
         T.p2 = mk(t.p[2][0], t.p[2][1], t.p[2][2]);
@@ -73,25 +81,34 @@ void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density) {
         T.absorb = (t.kd[0] == 0 && t.kd[1] == 0 && t.kd[2] == 0) ? 1 : 0;
         T.emit = t.emit != 0;
         if (T.emit) {
-            d.light_tri[nl] = i;
+            out->light_tri.push_back(i);
             // DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:64-66), .y()
             float pw[3];
             for (int k = 0; k < 3; ++k) pw[k] = ((T.Le[k] * 1.f) * T.area) * kPi;
-            d.light_func[nl] = lum3(pw);
-            ++nl;
+            out->light_func.push_back(lum3(pw));
         }
     }
+    const int nl = (int)out->light_tri.size();
     d.n_lights = nl;
     // Distribution1D(func, n) (sampling.h:57-69)
-    d.light_cdf[0] = 0;
-    for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] = d.light_cdf[i - 1] + d.light_func[i - 1] / (float)nl;
-    d.light_func_int = d.light_cdf[nl];
+    std::vector<float> &cdf = out->light_cdf;
+    const std::vector<float> &func = out->light_func;
+    cdf.assign((size_t)nl + 1, 0.f);
+    for (int i = 1; i < nl + 1; ++i) cdf[(size_t)i] = cdf[(size_t)i - 1] + func[(size_t)i - 1] / (float)nl;
+    d.light_func_int = cdf[(size_t)nl];
     if (d.light_func_int == 0) {
-        for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] = (float)i / (float)nl;
+        for (int i = 1; i < nl + 1; ++i) cdf[(size_t)i] = (float)i / (float)nl;
     } else {
-        for (int i = 1; i < nl + 1; ++i) d.light_cdf[i] /= d.light_func_int;
+        for (int i = 1; i < nl + 1; ++i) cdf[(size_t)i] /= d.light_func_int;
     }
-    *out = d;
+    out->depth = build_scene_bvh(out->tris, &out->nodes, &out->prims);
+    d.n_nodes = (int)out->nodes.size();
+}
+
+void prepare_scene(const bre_scene *s, HostScene *out, const float *d_density) {
+    out->head = DevScene{};
+    prepare_geometry(s, out);
+    prepare_medium(s, &out->head, d_density);
 }
 
 namespace {

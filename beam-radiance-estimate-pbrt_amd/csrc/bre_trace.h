@@ -153,17 +153,32 @@ struct PTri {
     int emit;    // a DiffuseAreaLight
 };
 
+// One node of the scene's bounding volume hierarchy: the reference's BVHAccel LinearBVHNode
+// (src/accelerators/bvh.cpp, 32 B, depth-first order: an interior node's first child follows it).
+struct SceneNode {
+    float lo[3], hi[3];  // Bounds3f
+    int32_t offset;      // leaf: primitivesOffset; interior: secondChildOffset
+    uint16_t nprims;     // 0 for an interior node
+    uint8_t axis;        // interior: split axis
+    uint8_t pad;
+};
+static_assert(sizeof(SceneNode) == 32, "SceneNode is BVHAccel's 32-B LinearBVHNode");
+constexpr int kSceneStack = 64;  // BVHAccel::Intersect's nodesToVisit[64]
+
 struct DevScene {
-    int n_tris, n_lights, medium, pad;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
+    int n_tris, n_lights, medium, n_nodes;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
     float sigma_t[3];
     float g;
-    // scene.lights (the emitting triangles, in order) and the Distribution1D of their Power().y()
-    // (ComputeLightPowerDistribution, integrator.cpp:217-225; sampling.h:55-69)
-    int light_tri[BRE_MAX_TRIANGLES];
-    float light_func[BRE_MAX_TRIANGLES];
-    float light_cdf[BRE_MAX_TRIANGLES + 1];
+    // the triangles in scene order, the BVHAccel over them (nodes + primitive order) and
+    // scene.lights (the emitting triangles, in order) with the Distribution1D of their Power().y()
+    // (ComputeLightPowerDistribution, integrator.cpp:217-225; sampling.h:55-69): device arrays
+    const PTri *t;
+    const SceneNode *nodes;
+    const int32_t *prims;       // BVH primitive slot -> triangle index
+    const int32_t *light_tri;
+    const float *light_func;
+    const float *light_cdf;     // n_lights + 1
     float light_func_int;
-    PTri t[BRE_MAX_TRIANGLES];
     // GridDensityMedium (grid.h:50-80): sigma_t = (sigma_a + sigma_s)[0], invMaxDensity
     int gn[3];
     float grid_sigma_t, grid_inv_max;
@@ -171,9 +186,30 @@ struct DevScene {
     const float *density;     // device copy of the grid (nx*ny*nz)
 };
 
-// host: derive the per-triangle constants and the light distribution exactly as
+// Host side of the scene: everything prepare_scene derives, in host memory; the context uploads
+// the arrays and points the DevScene at them.
+struct HostScene {
+    DevScene head;  // scalars; the array pointers are filled after the upload
+    std::vector<PTri> tris;
+    std::vector<SceneNode> nodes;
+    std::vector<int32_t> prims;
+    std::vector<int32_t> light_tri;
+    std::vector<float> light_func, light_cdf;
+    int depth = 0;  // deepest node of the BVH (root = 1)
+};
+
+// host: derive the per-triangle constants, the light distribution and the scene BVH exactly as
 // oracle/ora_pbrt.h make_scene does; `d_density` is the device copy of s->grid_density (grid media)
-void prepare_scene(const bre_scene *s, DevScene *out, const float *d_density = nullptr);
+void prepare_scene(const bre_scene *s, HostScene *out, const float *d_density = nullptr);
+// the two halves of prepare_scene: the triangles, lights and BVH (out->head's geometry fields and
+// the arrays), and the medium fields of a DevScene
+void prepare_geometry(const bre_scene *s, HostScene *out);
+void prepare_medium(const bre_scene *s, DevScene *d, const float *d_density);
+// host: the scene's BVHAccel (bvh.cpp: SAH, 12 buckets, maxPrimsInNode 4, depth-first layout) over
+// the triangles' world bounds; returns the tree depth
+int build_scene_bvh(const std::vector<PTri> &tris, std::vector<SceneNode> *nodes, std::vector<int32_t> *prims);
+// the scene's triangle array: the inline one or triangles_ext (bre_scene.h)
+inline const bre_triangle *scene_triangles(const bre_scene *s) { return s->triangles_ext ? s->triangles_ext : s->triangles; }
 // host: GridDensityMedium ctor's maxDensity loop (grid.h:73-76), std::max order
 float grid_max_density(const bre_scene *s);
 
@@ -246,19 +282,49 @@ __device__ __forceinline__ bool intersect_tri(const PTri &T, f3 o, f3 dir, float
     return true;
 }
 
-// Scene::Intersect over the triangles in order: each hit shrinks tMax (primitive.cpp:97-101); the
-// reference's BVH order only decides exact ties (here the later triangle of equal t wins)
+// Scene::Intersect = BVHAccel::Intersect (bvh.cpp): depth-first through the scene BVH, near child
+// first by dirIsNeg[axis], every node tested with the reference's slab test against the CURRENT
+// tMax, every leaf triangle with Triangle::Intersect, each hit shrinking tMax (primitive.cpp:97-101).
+// The triangles are tested in the reference's order, so among equal-t hits the same one wins.  The
+// host checks the tree depth against kSceneStack (prepare_scene), so the stack cannot overflow.
 __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, float &tmax, Hit &h) {
+    const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
+    const int n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
+    int stack[kSceneStack];
+    int sp = 0, cur = 0;
     bool hit = false;
-    for (int i = 0; i < S.n_tris; ++i) {
-        float t;
-        Hit tmp;
-        if (!intersect_tri(S.t[i], o, d, tmax, t, tmp)) continue;
-        tmax = t;
-        h.p = tmp.p;
-        h.perr = tmp.perr;
-        h.tri = i;
-        hit = true;
+    while (true) {
+        const SceneNode &nd = S.nodes[cur];
+        const Box6 b{nd.lo[0], nd.lo[1], nd.lo[2], nd.hi[0], nd.hi[1], nd.hi[2]};
+        if (slab_test(b, o, inv, n0, n1, n2, tmax, nullptr)) {
+            if (nd.nprims > 0) {
+                for (int i = 0; i < nd.nprims; ++i) {
+                    const int ti = S.prims[nd.offset + i];
+                    float t;
+                    Hit tmp;
+                    if (!intersect_tri(S.t[ti], o, d, tmax, t, tmp)) continue;
+                    tmax = t;
+                    h.p = tmp.p;
+                    h.perr = tmp.perr;
+                    h.tri = ti;
+                    hit = true;
+                }
+                if (sp == 0) break;
+                cur = stack[--sp];
+            } else {
+                const int neg = nd.axis == 0 ? n0 : (nd.axis == 1 ? n1 : n2);
+                if (neg) {
+                    stack[sp++] = cur + 1;
+                    cur = nd.offset;
+                } else {
+                    stack[sp++] = nd.offset;
+                    cur = cur + 1;
+                }
+            }
+        } else {
+            if (sp == 0) break;
+            cur = stack[--sp];
+        }
     }
     return hit;
 }

@@ -14,7 +14,7 @@ struct bre_pbrt {
 
 static bre_status finish_parse(bre_pbrt *p, bool ok) {
     p->ok = ok;
-    if (ok && p->scene.scene.has_medium == BRE_MEDIUM_GRID) p->scene.scene.grid_density = p->scene.density.data();
+    if (ok) p->scene.Bind();
     return ok ? BRE_OK : BRE_ERR_INVALID_ARG;
 }
 

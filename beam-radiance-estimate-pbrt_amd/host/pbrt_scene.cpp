@@ -1081,8 +1081,8 @@ bool Parser::Finish() {
     };
     if (!o.haveCamera) return fatal("no usable perspective Camera");
     if (shapes_.empty()) return fatal("the scene has no shapes");
-    if ((int)shapes_.size() > BRE_MAX_TRIANGLES)
-        return fatal("more than BRE_MAX_TRIANGLES (" + std::to_string(BRE_MAX_TRIANGLES) + ") triangles");
+    if ((int64_t)shapes_.size() > BRE_MAX_SCENE_TRIANGLES)
+        return fatal("more than BRE_MAX_SCENE_TRIANGLES (" + std::to_string(BRE_MAX_SCENE_TRIANGLES) + ") triangles");
     int nemit = 0;
     for (size_t i = 0; i < shapes_.size(); ++i) nemit += shapes_[i].tri.emit != 0;
     if (nemit == 0) return fatal("the scene has no diffuse area light");
@@ -1108,7 +1108,13 @@ bool Parser::Finish() {
     bre_scene &sc = o.scene;
     memset(&sc, 0, sizeof(sc));
     sc.n_triangles = (int32_t)shapes_.size();
-    for (size_t i = 0; i < shapes_.size(); ++i) sc.triangles[i] = shapes_[i].tri;
+    // up to BRE_MAX_TRIANGLES inline, any number through triangles_ext (PbrtScene::triangles)
+    if (shapes_.size() <= (size_t)BRE_MAX_TRIANGLES) {
+        for (size_t i = 0; i < shapes_.size(); ++i) sc.triangles[i] = shapes_[i].tri;
+    } else {
+        o.triangles.resize(shapes_.size());
+        for (size_t i = 0; i < shapes_.size(); ++i) o.triangles[i] = shapes_[i].tri;
+    }
     if (med) {
         sc.has_medium = med->kind;
         memcpy(sc.sigma_a, med->sigma_a, sizeof(sc.sigma_a));
@@ -1125,12 +1131,17 @@ bool Parser::Finish() {
     memcpy(sc.cam_look, camLook_ + 3, 12);
     memcpy(sc.cam_up, camLook_ + 6, 12);
     sc.cam_fov_deg = camFov_;
-    sc.grid_density = o.density.empty() ? nullptr : o.density.data();
+    o.Bind();
     if (o.integratorName.empty()) o.integratorName = "path";  // pbrt's default integrator
     return true;
 }
 
 }  // namespace
+
+void PbrtScene::Bind() {
+    scene.grid_density = density.empty() ? nullptr : density.data();
+    scene.triangles_ext = triangles.empty() ? nullptr : triangles.data();
+}
 
 static bool ParseLexer(Lexer &lx, PbrtScene *out) {
     *out = PbrtScene();

@@ -16,7 +16,8 @@
 // else is reported with pbrt-style Error()/Warning() text and the offending statement skipped:
 //   * Shape "trianglemesh" -> one bre_triangle per index triple (vertices through the CTM exactly
 //     as TriangleMesh does, mesh->p[i] = ObjectToWorld(P[i]), shapes/triangle.cpp; flip =
-//     ReverseOrientation ^ TransformSwapsHandedness); up to BRE_MAX_TRIANGLES.
+//     ReverseOrientation ^ TransformSwapsHandedness); any number up to BRE_MAX_SCENE_TRIANGLES (more
+//     than BRE_MAX_TRIANGLES go through bre_scene.triangles_ext).
 //   * Material "matte" with "Kd" (rgb, default 0.5) and sigma 0; MakeNamedMaterial/NamedMaterial.
 //   * AreaLightSource "diffuse" ("L" x "scale", one-sided): every triangle of an emitting mesh is
 //     its own light, as pbrtShape makes one DiffuseAreaLight per shape (api.cpp).
@@ -104,8 +105,11 @@ struct FilmDesc {
 
 // Everything the render needs from one .pbrt file.
 struct PbrtScene {
-    bre_scene scene;                  // grid_density points into `density` below
+    bre_scene scene;                  // grid_density / triangles_ext point into the vectors below
     std::vector<float> density;       // heterogeneous medium data (nx*ny*nz)
+    std::vector<bre_triangle> triangles;  // the triangles when there are more than BRE_MAX_TRIANGLES
+    // Re-point scene.grid_density / scene.triangles_ext at this object's vectors (after a copy).
+    void Bind();
     FilmDesc film;
     std::string integratorName;       // "photonbeam" expected
     ParamSet integratorParams;        // CreatePhotonBeamIntegrator's ParamSet

@@ -8,7 +8,8 @@ from __future__ import annotations
 
 import ctypes
 
-MAX_TRIANGLES = 128
+MAX_TRIANGLES = 128               # inline in Scene.triangles
+MAX_SCENE_TRIANGLES = 1 << 24     # through Scene.triangles_ext
 MAX_DEPTH = 16
 MEDIUM_NONE, MEDIUM_HOMOGENEOUS, MEDIUM_GRID = 0, 1, 2
 
@@ -26,7 +27,7 @@ class Scene(ctypes.Structure):
                 ("cam_pos", F3), ("cam_look", F3), ("cam_up", F3), ("cam_fov_deg", ctypes.c_float),
                 ("triangles", Triangle * MAX_TRIANGLES),
                 ("grid_n", ctypes.c_int32 * 3), ("world_to_medium", ctypes.c_float * 16),
-                ("grid_density", ctypes.c_void_p)]
+                ("grid_density", ctypes.c_void_p), ("triangles_ext", ctypes.c_void_p)]
 
     def to_bytes(self) -> bytes:
         return ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self))
@@ -57,15 +58,19 @@ def make_scene(meshes, sigma_a=None, sigma_s=None, g=0.0,
                cam_pos=(0.5, 0.5, 0.02), cam_look=(0.5, 0.5, 1.0), cam_up=(0.0, 1.0, 0.0), fov=60.0) -> Scene:
     """meshes: list of (P, indices, kd, Le) -- a pbrt "trianglemesh" with world-space points P
     (list of xyz), index triples, Lambertian kd, and Le (None = not emitting); medium present iff
-    sigma_a is given (RGB or scalar)."""
+    sigma_a is given (RGB or scalar).  More than MAX_TRIANGLES triangles go to an external array
+    (Scene.triangles_ext, kept alive on the scene object)."""
     s = Scene()
     ctypes.memset(ctypes.addressof(s), 0, ctypes.sizeof(s))
+    total = sum(len(idx) // 3 for _, idx, _, _ in meshes)
+    assert total <= MAX_SCENE_TRIANGLES
+    ext = (Triangle * total)() if total > MAX_TRIANGLES else None
+    dst = ext if ext is not None else s.triangles
     n = 0
     for P, idx, kd, Le in meshes:
         assert len(idx) % 3 == 0
         for t in range(len(idx) // 3):
-            assert n < MAX_TRIANGLES
-            T = s.triangles[n]
+            T = dst[n]
             for v in range(3):
                 T.p[v] = _f3(P[idx[3 * t + v]])
             T.kd = _f3(kd)
@@ -74,6 +79,9 @@ def make_scene(meshes, sigma_a=None, sigma_s=None, g=0.0,
                 T.Le = _f3(Le)
             n += 1
     s.n_triangles = n
+    if ext is not None:
+        s.triangles_ext = ctypes.addressof(ext)
+        s._triangles_ref = ext
     if sigma_a is not None:
         rgb = (lambda v: (v, v, v) if isinstance(v, (int, float)) else tuple(v))
         s.has_medium = 1
@@ -109,6 +117,43 @@ def cornell_meshes(light_L=(17.0, 12.0, 4.0)):
 def cornell_scene(sigma_a: float = 0.05, sigma_s: float = 0.5, g: float = 0.0) -> Scene:
     """Cornell box in homogeneous fog (sigma_a 0.05, sigma_s 0.5, g 0)."""
     return make_scene(cornell_meshes(), sigma_a, sigma_s, g)
+
+
+def uv_sphere(center=(0.5, 0.35, 0.55), radius=0.2, n_theta=64, n_phi=96):
+    """A triangulated sphere as one pbrt "trianglemesh": (points, indices) with n_theta rings and
+    n_phi segments, outward-facing (counter-clockwise seen from outside), poles shared:
+    2 * n_phi * (n_theta - 1) triangles (12,096 at the defaults)."""
+    import numpy as np
+
+    cx, cy, cz = (float(v) for v in center)
+    pts = [(cx, cy + radius, cz)]
+    for t in range(1, n_theta):
+        th = np.pi * t / n_theta
+        for k in range(n_phi):
+            ph = 2 * np.pi * k / n_phi
+            pts.append((cx + radius * np.sin(th) * np.cos(ph), cy + radius * np.cos(th), cz + radius * np.sin(th) * np.sin(ph)))
+    pts.append((cx, cy - radius, cz))
+    ring = lambda t, k: 1 + (t - 1) * n_phi + (k % n_phi)  # noqa: E731
+    idx = []
+    for k in range(n_phi):
+        idx += [0, ring(1, k + 1), ring(1, k)]
+    for t in range(1, n_theta - 1):
+        for k in range(n_phi):
+            a, b, c, d = ring(t, k), ring(t, k + 1), ring(t + 1, k), ring(t + 1, k + 1)
+            idx += [a, b, d, a, d, c]
+    south = len(pts) - 1
+    for k in range(n_phi):
+        idx += [south, ring(n_theta - 1, k), ring(n_theta - 1, k + 1)]
+    return [tuple(np.float32(c) for c in p) for p in pts], idx
+
+
+def cornell_sphere_scene(sigma_a: float = 0.05, sigma_s: float = 0.5, g: float = 0.0, n_theta=64, n_phi=96) -> Scene:
+    """The C1/C2 Cornell box in fog with a white tessellated sphere (uv_sphere, 12,096 triangles at
+    the defaults) on the floor side: a scene far past the 128 inline triangles, through
+    Scene.triangles_ext and the scene BVH (bvh.cpp BVHAccel)."""
+    P, idx = uv_sphere(n_theta=n_theta, n_phi=n_phi)
+    meshes = cornell_meshes()
+    return make_scene(meshes[:-1] + [(P, idx, (0.6, 0.6, 0.6), None)] + meshes[-1:], sigma_a, sigma_s, g)
 
 
 def smoke_density(n: int = 64, seed: int = 7):

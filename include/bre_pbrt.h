@@ -38,8 +38,9 @@ bre_status bre_pbrt_parse_string(const char *text, bre_pbrt **out);
 void bre_pbrt_free(bre_pbrt *p);
 /* Error()/Warning() text, one message per line; counts may be NULL. */
 const char *bre_pbrt_messages(const bre_pbrt *p, int32_t *n_errors, int32_t *n_warnings);
-/* The scene for bre_trace_photons / bre_camera_pass / bre_render; grid_density points into the
-   parsed scene and stays valid until bre_pbrt_free. */
+/* The scene for bre_trace_photons / bre_camera_pass / bre_render; grid_density and (for more than
+   BRE_MAX_TRIANGLES triangles) triangles_ext point into the parsed scene and stay valid until
+   bre_pbrt_free. */
 bre_status bre_pbrt_get_scene(const bre_pbrt *p, bre_scene *out);
 /* CreatePhotonBeamIntegrator's parameters for the film of the scene (quick != 0 is pbrt's
    --quick); *write_frequency (may be NULL) receives "imagewritefrequency" as given (default 1 << 31 =

@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define BRE_MAX_TRIANGLES 128
+#define BRE_MAX_TRIANGLES 128               /* triangles held inline in bre_scene.triangles */
+#define BRE_MAX_SCENE_TRIANGLES (1 << 24)  /* triangles through bre_scene.triangles_ext */
 #define BRE_MAX_DEPTH 16 /* maxdepth accepted by the photon / camera passes */
 
 #define BRE_MEDIUM_NONE 0
@@ -59,7 +60,8 @@ typedef struct bre_triangle {
 } bre_triangle;
 
 typedef struct bre_scene {
-    int32_t n_triangles;   /* 1 .. BRE_MAX_TRIANGLES; at least one with emit != 0 */
+    int32_t n_triangles;   /* 1 .. BRE_MAX_TRIANGLES inline, or 1 .. BRE_MAX_SCENE_TRIANGLES through
+                              triangles_ext; at least one with emit != 0 */
     int32_t has_medium;    /* BRE_MEDIUM_NONE (vacuum) / _HOMOGENEOUS / _GRID, filling all space */
     float sigma_a[3];      /* medium sigma_a (already multiplied by "scale") */
     float sigma_s[3];      /* medium sigma_s */
@@ -76,6 +78,13 @@ typedef struct bre_scene {
                                    Scale(p1 - p0)), row-major 4x4 (grid.h:58) */
     const float *grid_density;  /* nx*ny*nz densities, index (z*ny + y)*nx + x (grid.h:84-88);
                                    caller-owned host memory, read during the call */
+    /* Any number of triangles (BRE_MAX_SCENE_TRIANGLES): when non-NULL, the scene's triangles are
+       triangles_ext[0 .. n_triangles) (caller-owned host memory, read during the call) and the
+       inline array is unused.  Either way the passes intersect the scene through pbrt's BVHAccel
+       (src/accelerators/bvh.cpp: SAH, 12 buckets, maxnodeprims 4 -- the "bvh" accelerator's
+       defaults, CreateBVHAccelerator), built on the host over the triangles in scene order, so
+       equal-distance hits resolve in the reference's order. */
+    const bre_triangle *triangles_ext;
 } bre_scene;
 
 /* PhotonBeamIntegrator parameters (CreatePhotonBeamIntegrator, photonbeam.cpp:589-611). */

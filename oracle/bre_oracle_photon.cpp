@@ -334,6 +334,41 @@ void ora_tri_hits(const bre_scene *scene, int64_t n, const float *o, const float
     }
 }
 
+// Scene::Intersect for n rays (o, d, tMax = +inf): through the scene's BVHAccel (use_bvh != 0, what
+// the passes use) or over the triangles in scene order (the round-2 restatement); the hit distance
+// (the final ray.tMax, +inf for a miss) and triangle (-1 for a miss).  *depth: the BVH's depth.
+void ora_scene_intersect(const bre_scene *scene, int64_t n, const float *o, const float *d, int32_t use_bvh,
+                         float *t_out, int32_t *tri_out, int32_t *depth) {
+    orp::Scene sc = orp::make_scene(scene);
+    for (int64_t i = 0; i < n; ++i) {
+        orp::Ray r;
+        r.o = orp::V3(o + 3 * i);
+        r.d = orp::V3(d + 3 * i);
+        r.tMax = orp::Infinity;
+        orp::Isect is;
+        const bool hit = use_bvh ? orp::Intersect(sc, r, &is) : orp::IntersectLinear(sc, r, &is);
+        t_out[i] = r.tMax;
+        tri_out[i] = hit ? is.tri : -1;
+    }
+    if (depth) {
+        // depth of the flattened tree: walk it with an explicit stack of (node, level)
+        int best = 0;
+        std::vector<std::pair<int, int>> st;
+        if (!sc.nodes.empty()) st.push_back({0, 1});
+        while (!st.empty()) {
+            const auto [k, lv] = st.back();
+            st.pop_back();
+            best = std::max(best, lv);
+            const orp::LinearBVHNode &nd = sc.nodes[(size_t)k];
+            if (nd.nPrimitives == 0) {
+                st.push_back({k + 1, lv + 1});
+                st.push_back({nd.offset, lv + 1});
+            }
+        }
+        *depth = best;
+    }
+}
+
 // Triangle::Sample(u) (triangle.cpp:543-568, area measure) of triangle `tri` for n sample pairs
 void ora_tri_sample(const bre_scene *scene, int32_t tri, int64_t n, const float *u, float *p, float *nrm,
                     float *pdf) {

@@ -6,6 +6,8 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
+#include <memory>
 #include <vector>
 
 #include "../include/bre_fmath.h"
@@ -303,8 +305,19 @@ struct Distribution1D {
     }
 };
 
+// BVHAccel (src/accelerators/bvh.cpp): the scene's aggregate.  LinearBVHNode (bvh.cpp) in
+// depth-first order: an interior node's first child follows it, the second is at secondChildOffset.
+struct LinearBVHNode {
+    V3 pMin, pMax;
+    int offset;       // primitivesOffset (leaf) / secondChildOffset (interior)
+    int nPrimitives;  // 0: interior
+    int axis;
+};
+
 struct Scene {
     std::vector<Tri> tris;
+    std::vector<LinearBVHNode> nodes;  // BVHAccel over tris (CreateBVHAccelerator defaults)
+    std::vector<int> orderedPrims;     // BVHAccel::primitives after the build: triangle indices
     std::vector<int> lights;  // scene.lights: the emitting triangles, in triangle order
     // ComputeLightPowerDistribution (integrator.cpp:217-225) -> Distribution1D (sampling.h:55-100)
     Distribution1D ldist;
@@ -322,10 +335,176 @@ struct Scene {
 // the light-power distribution's SampleDiscrete (Distribution1D above)
 static int SampleDiscrete(const Scene &sc, Float u, Float *pdf) { return sc.ldist.SampleDiscrete(u, pdf); }
 
+// ---- BVHAccel (bvh.cpp), restated: recursiveBuild with SplitMethod::SAH, maxPrimsInNode 4 ----
+struct Bounds3f {
+    V3 pMin = V3(std::numeric_limits<Float>::max(), std::numeric_limits<Float>::max(),
+                 std::numeric_limits<Float>::max());
+    V3 pMax = V3(std::numeric_limits<Float>::lowest(), std::numeric_limits<Float>::lowest(),
+                 std::numeric_limits<Float>::lowest());
+    int MaximumExtent() const {
+        const V3 d = pMax - pMin;
+        if (d.x > d.y && d.x > d.z) return 0;
+        else if (d.y > d.z) return 1;
+        else return 2;
+    }
+    Float SurfaceArea() const {
+        const V3 d = pMax - pMin;
+        return 2 * (d.x * d.y + d.x * d.z + d.y * d.z);
+    }
+    V3 Offset(const V3 &p) const {
+        V3 o = p - pMin;
+        if (pMax.x > pMin.x) o.x /= pMax.x - pMin.x;
+        if (pMax.y > pMin.y) o.y /= pMax.y - pMin.y;
+        if (pMax.z > pMin.z) o.z /= pMax.z - pMin.z;
+        return o;
+    }
+};
+static inline Bounds3f Union(const Bounds3f &b, const V3 &p) {
+    Bounds3f r;
+    r.pMin = V3(std::min(b.pMin.x, p.x), std::min(b.pMin.y, p.y), std::min(b.pMin.z, p.z));
+    r.pMax = V3(std::max(b.pMax.x, p.x), std::max(b.pMax.y, p.y), std::max(b.pMax.z, p.z));
+    return r;
+}
+static inline Bounds3f Union(const Bounds3f &a, const Bounds3f &b) {
+    Bounds3f r;
+    r.pMin = V3(std::min(a.pMin.x, b.pMin.x), std::min(a.pMin.y, b.pMin.y), std::min(a.pMin.z, b.pMin.z));
+    r.pMax = V3(std::max(a.pMax.x, b.pMax.x), std::max(a.pMax.y, b.pMax.y), std::max(a.pMax.z, b.pMax.z));
+    return r;
+}
+struct BVHPrimitiveInfo {
+    size_t primitiveNumber;
+    Bounds3f bounds;
+    V3 centroid;
+};
+struct BVHBuildNode {
+    Bounds3f bounds;
+    BVHBuildNode *children[2] = {nullptr, nullptr};
+    int splitAxis = 0, firstPrimOffset = 0, nPrimitives = 0;
+};
+struct BVHBuilder {
+    std::vector<BVHPrimitiveInfo> &info;
+    std::vector<int> &orderedPrims;
+    std::vector<std::unique_ptr<BVHBuildNode>> arena;
+    int totalNodes = 0;
+    BVHBuildNode *leaf(int start, int end, const Bounds3f &bounds) {
+        BVHBuildNode *node = arena.back().get();
+        node->firstPrimOffset = (int)orderedPrims.size();
+        for (int i = start; i < end; ++i) orderedPrims.push_back((int)info[i].primitiveNumber);
+        node->nPrimitives = end - start;
+        node->bounds = bounds;
+        return node;
+    }
+    BVHBuildNode *build(int start, int end) {  // recursiveBuild
+        arena.emplace_back(new BVHBuildNode());
+        BVHBuildNode *node = arena.back().get();
+        ++totalNodes;
+        Bounds3f bounds;
+        for (int i = start; i < end; ++i) bounds = Union(bounds, info[i].bounds);
+        const int nPrimitives = end - start;
+        if (nPrimitives == 1) return leaf(start, end, bounds);
+        Bounds3f centroidBounds;
+        for (int i = start; i < end; ++i) centroidBounds = Union(centroidBounds, info[i].centroid);
+        const int dim = centroidBounds.MaximumExtent();
+        int mid = (start + end) / 2;
+        if (centroidBounds.pMax[dim] == centroidBounds.pMin[dim]) return leaf(start, end, bounds);
+        if (nPrimitives <= 2) {
+            mid = (start + end) / 2;
+            std::nth_element(&info[start], &info[mid], &info[end - 1] + 1,
+                             [dim](const BVHPrimitiveInfo &a, const BVHPrimitiveInfo &b) {
+                                 return a.centroid[dim] < b.centroid[dim];
+                             });
+        } else {
+            const int nBuckets = 12;
+            int count[12] = {};
+            Bounds3f bb[12];
+            for (int i = start; i < end; ++i) {
+                int b = nBuckets * centroidBounds.Offset(info[i].centroid)[dim];
+                if (b == nBuckets) b = nBuckets - 1;
+                count[b]++;
+                bb[b] = Union(bb[b], info[i].bounds);
+            }
+            Float cost[11];
+            for (int i = 0; i < nBuckets - 1; ++i) {
+                Bounds3f b0, b1;
+                int count0 = 0, count1 = 0;
+                for (int j = 0; j <= i; ++j) {
+                    b0 = Union(b0, bb[j]);
+                    count0 += count[j];
+                }
+                for (int j = i + 1; j < nBuckets; ++j) {
+                    b1 = Union(b1, bb[j]);
+                    count1 += count[j];
+                }
+                cost[i] = 1 + (count0 * b0.SurfaceArea() + count1 * b1.SurfaceArea()) / bounds.SurfaceArea();
+            }
+            Float minCost = cost[0];
+            int minCostSplitBucket = 0;
+            for (int i = 1; i < nBuckets - 1; ++i)
+                if (cost[i] < minCost) {
+                    minCost = cost[i];
+                    minCostSplitBucket = i;
+                }
+            const Float leafCost = nPrimitives;
+            const int maxPrimsInNode = 4;
+            if (nPrimitives > maxPrimsInNode || minCost < leafCost) {
+                BVHPrimitiveInfo *pmid = std::partition(&info[start], &info[end - 1] + 1, [=](const BVHPrimitiveInfo &pi) {
+                    int b = nBuckets * centroidBounds.Offset(pi.centroid)[dim];
+                    if (b == nBuckets) b = nBuckets - 1;
+                    return b <= minCostSplitBucket;
+                });
+                mid = (int)(pmid - &info[0]);
+            } else {
+                return leaf(start, end, bounds);
+            }
+        }
+        BVHBuildNode *c0 = build(start, mid);
+        BVHBuildNode *c1 = build(mid, end);
+        node->children[0] = c0;
+        node->children[1] = c1;
+        node->bounds = Union(c0->bounds, c1->bounds);  // InitInterior
+        node->splitAxis = dim;
+        node->nPrimitives = 0;
+        return node;
+    }
+};
+static int flattenBVHTree(const BVHBuildNode *node, std::vector<LinearBVHNode> &nodes) {  // flattenBVHTree
+    const int myOffset = (int)nodes.size();
+    nodes.push_back(LinearBVHNode{node->bounds.pMin, node->bounds.pMax, 0, node->nPrimitives, 0});
+    if (node->nPrimitives > 0) {
+        nodes[myOffset].offset = node->firstPrimOffset;
+    } else {
+        nodes[myOffset].axis = node->splitAxis;
+        flattenBVHTree(node->children[0], nodes);
+        nodes[myOffset].offset = flattenBVHTree(node->children[1], nodes);
+    }
+    return myOffset;
+}
+// BVHAccel ctor over the scene's triangles in order (Triangle::WorldBound: Union(Bounds3f(p0, p1), p2))
+static void BuildSceneBVH(Scene &sc) {
+    std::vector<BVHPrimitiveInfo> info(sc.tris.size());
+    for (size_t i = 0; i < sc.tris.size(); ++i) {
+        const Tri &T = sc.tris[i];
+        Bounds3f b;
+        b.pMin = V3(std::min(T.p0.x, T.p1.x), std::min(T.p0.y, T.p1.y), std::min(T.p0.z, T.p1.z));
+        b.pMax = V3(std::max(T.p0.x, T.p1.x), std::max(T.p0.y, T.p1.y), std::max(T.p0.z, T.p1.z));
+        b = Union(b, T.p2);
+        info[i].primitiveNumber = i;
+        info[i].bounds = b;
+        info[i].centroid = b.pMin * .5f + b.pMax * .5f;  // .5f * pMin + .5f * pMax
+    }
+    sc.nodes.clear();
+    sc.orderedPrims.clear();
+    if (info.empty()) return;
+    BVHBuilder bld{info, sc.orderedPrims, {}, 0};
+    BVHBuildNode *root = bld.build(0, (int)info.size());
+    flattenBVHTree(root, sc.nodes);
+}
+
 static Scene make_scene(const bre_scene *s) {
     Scene sc;
+    const bre_triangle *tri = s->triangles_ext ? s->triangles_ext : s->triangles;
     for (int i = 0; i < s->n_triangles; ++i) {
-        const bre_triangle &t = s->triangles[i];
+        const bre_triangle &t = tri[i];
         Tri T;
         T.p0 = V3(t.p[0]);
         T.p1 = V3(t.p[1]);
@@ -356,6 +535,7 @@ static Scene make_scene(const bre_scene *s) {
         lfunc.push_back(((T.Le * (Float)1) * T.area * Pi).y());
     }
     if (!lfunc.empty()) sc.ldist = Distribution1D(lfunc.data(), (int)lfunc.size());
+    BuildSceneBVH(sc);
     sc.medium = s->has_medium != 0;
     Spectrum sa(s->sigma_a);
     sc.sigma_s = Spectrum(s->sigma_s);
@@ -379,7 +559,7 @@ static Scene make_scene(const bre_scene *s) {
 
 struct Isect {
     V3 p, pError, n;
-    int tri;
+    int tri = -1;
 };
 
 static inline int MaxDimension(const V3 &v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
@@ -456,10 +636,73 @@ static bool IntersectTri(const Tri &T, const Ray &ray, Float *tHit, Isect *isect
     return true;
 }
 
-// Scene::Intersect over the triangles in order (GeometricPrimitive::Intersect sets ray.tMax to the
-// hit, primitive.cpp:97-101; the reference's BVH order decides only exact ties, where the later
-// triangle of equal t wins here).
+// Bounds3::IntersectP(ray, invDir, dirIsNeg), geometry.h:1410-1436
+static inline bool IntersectP(const LinearBVHNode &b, const Ray &ray, const V3 &invDir, const int dirIsNeg[3]) {
+    const V3 bnd[2] = {b.pMin, b.pMax};
+    Float tMin = (bnd[dirIsNeg[0]].x - ray.o.x) * invDir.x;
+    Float tMax = (bnd[1 - dirIsNeg[0]].x - ray.o.x) * invDir.x;
+    Float tyMin = (bnd[dirIsNeg[1]].y - ray.o.y) * invDir.y;
+    Float tyMax = (bnd[1 - dirIsNeg[1]].y - ray.o.y) * invDir.y;
+    tMax *= 1 + 2 * gamma(3);
+    tyMax *= 1 + 2 * gamma(3);
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    Float tzMin = (bnd[dirIsNeg[2]].z - ray.o.z) * invDir.z;
+    Float tzMax = (bnd[1 - dirIsNeg[2]].z - ray.o.z) * invDir.z;
+    tzMax *= 1 + 2 * gamma(3);
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    return (tMin < ray.tMax) && (tMax > 0);
+}
+
+// Scene::Intersect = BVHAccel::Intersect (bvh.cpp): depth first, near child first by dirIsNeg[axis];
+// every hit shrinks ray.tMax (GeometricPrimitive::Intersect, primitive.cpp:97-101), so an
+// equal-distance tie goes to the triangle the reference tests last.
 static bool Intersect(const Scene &sc, Ray &ray, Isect *isect) {
+    if (sc.nodes.empty()) return false;
+    bool hit = false;
+    const V3 invDir(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+    const int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    int toVisitOffset = 0, currentNodeIndex = 0;
+    int nodesToVisit[64];
+    while (true) {
+        const LinearBVHNode *node = &sc.nodes[currentNodeIndex];
+        if (IntersectP(*node, ray, invDir, dirIsNeg)) {
+            if (node->nPrimitives > 0) {
+                for (int i = 0; i < node->nPrimitives; ++i) {
+                    const int ti = sc.orderedPrims[node->offset + i];
+                    Float t;
+                    Isect tmp;
+                    if (!IntersectTri(sc.tris[ti], ray, &t, &tmp)) continue;
+                    ray.tMax = t;
+                    *isect = tmp;
+                    isect->tri = ti;
+                    hit = true;
+                }
+                if (toVisitOffset == 0) break;
+                currentNodeIndex = nodesToVisit[--toVisitOffset];
+            } else {
+                if (dirIsNeg[node->axis]) {
+                    nodesToVisit[toVisitOffset++] = currentNodeIndex + 1;
+                    currentNodeIndex = node->offset;
+                } else {
+                    nodesToVisit[toVisitOffset++] = node->offset;
+                    currentNodeIndex = currentNodeIndex + 1;
+                }
+            }
+        } else {
+            if (toVisitOffset == 0) break;
+            currentNodeIndex = nodesToVisit[--toVisitOffset];
+        }
+    }
+    return hit;
+}
+
+// The round-2 restatement (every triangle in scene order; a later triangle wins an exact tie):
+// kept for tests/refpy_photon.py's independent cross-check.
+static bool IntersectLinear(const Scene &sc, Ray &ray, Isect *isect) {
     bool hit = false;
     for (int i = 0; i < (int)sc.tris.size(); ++i) {
         Float t;

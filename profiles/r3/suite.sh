@@ -14,7 +14,7 @@ timeout -k 10 300 python -u bench.py --no-cpu --no-pmc --entry boundary --json-o
 for f in camera boundary; do
   python3 -c "import json;d=json.load(open('$OUT/bench_$f.json'));print('$f', 'value', round(d['value']), 'gather', round(d['gather_kernel_ms'],1), [round(x) for x in d['gather_ms_per_step'][::3]], 'q/est', round(d.get('queued_pairs_per_estimate',0)), 'tests/q', round(d.get('prefilter_tests_per_queued_pair',0),2))"
 done
-for it in 0 8; do
+for it in ${DEPTH_KEYS_ITERS:-}; do
   timeout -k 10 200 python -u profiles/r3/depth_keys.py c2 $it 1,2,3 > "$OUT/depth_keys_c2_$it.log" 2>&1 \
       || { tail -n 20 "$OUT/depth_keys_c2_$it.log"; exit 1; }
   grep -v '^{' "$OUT/depth_keys_c2_$it.log" | python3 -c "

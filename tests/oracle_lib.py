@@ -66,6 +66,7 @@ class Oracle:
         lib.ora_distribution1d.argtypes = [P, I32, I64, P, P, P, P, P]
         lib.ora_distribution1d_continuous.argtypes = [P, I32, I64, P, P, P, P]
         lib.ora_tri_reintersect.argtypes = [I32, I32, P, P]
+        lib.ora_scene_intersect.argtypes = [P, I64, P, P, I32, P, P, P]
         lib.ora_tri_reintersect.restype = I64
 
     # -- primitives --
@@ -163,6 +164,15 @@ class Oracle:
         out = np.zeros(o.shape[0], np.int32)
         self.lib.ora_tri_hits(ctypes.addressof(scene), o.shape[0], _p(o), _p(d), _p(out))
         return out
+
+    def scene_intersect(self, scene, o, d, bvh=True):
+        """Scene::Intersect per ray (tMax = inf): (t, triangle or -1, BVH depth)."""
+        o, d = (np.ascontiguousarray(x, np.float32) for x in (o, d))
+        n = o.shape[0]
+        t, tri, depth = np.zeros(n, np.float32), np.zeros(n, np.int32), ctypes.c_int32(0)
+        self.lib.ora_scene_intersect(ctypes.addressof(scene), n, _p(o), _p(d), int(bool(bvh)), _p(t), _p(tri),
+                                     ctypes.byref(depth))
+        return t, tri, depth.value
 
     def tri_sample(self, scene, tri, u):
         """Triangle::Sample(u) of triangle `tri` (area measure): points, normals, pdfs."""

@@ -99,3 +99,27 @@ def test_cli_renders_pfm(pb, tmp_path):
     img = pb.read_pfm(str(out))
     ref = pb.parse_string(SMALL).render(write_files=False)
     assert img.shape == ref.shape and _rel_l2(img, ref) <= 1e-6
+
+
+def test_big_mesh_pbrt_render_matches_oracle(bre, pb, oracle):
+    """12,110 triangles through the .pbrt front end (triangles_ext, the scene BVH on the GPU): the
+    render is within the north star's 1e-3 of the oracle chain."""
+    from test_pbrt_scene import sphere_pbrt
+
+    k = SMALL.rindex("AttributeBegin")
+    s = pb.parse_string(SMALL[:k] + sphere_pbrt() + SMALL[k:])
+    assert s.ok, s.messages
+    assert s.scene.n_triangles == 12110
+    w, h, p = s.film["xres"], s.film["yres"], s.params
+    img = s.render(write_files=False)
+    ld = np.zeros((w * h, 3))
+    for it in range(p.end_iteration):
+        R = np.float32(bre.beam_radius_at(p.initial_radius, p.alpha, it))
+        cam = oracle.camera_pass(s.scene, w, h, iteration=it, max_depth=p.max_depth)
+        ld += cam["surface"]
+        beams = oracle.trace_photons(s.scene, p.photons_per_iteration, iteration=it, max_depth=p.max_depth, radius=R)
+        out = oracle.build(beams).gather({k: cam[k] for k in ("o", "p", "d", "tmax", "pixel")}, R, npix=w * h)
+        ld += out["accum"]
+    ref = pb.film_finalize((ld / p.end_iteration).astype(np.float32))
+    assert img.mean() > 0
+    assert _rel_l2(img.reshape(-1, 3), ref) <= 1e-5
