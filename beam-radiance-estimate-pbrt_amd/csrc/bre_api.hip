@@ -70,7 +70,7 @@ struct bre_ctx {
     int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
-    int beam_key = 0;        // internal: beam sort key of the tree build (BuildBuffers::beam_key)
+    int beam_key = 1;        // internal: tree order of the build (BuildBuffers::beam_key): 1 (start, end), 0 centroid
     int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -87,7 +87,7 @@ struct bre_ctx {
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     int built_leaf_size = 1;
     DevMem in_start, in_end, in_radius, in_power;  // staging for host-pointer uploads
-    DevMem box, cent, cbounds, nvalid_buf, keys, keys_alt, vals, vals_alt, sort_tmp, leaf_parent, visit;
+    DevMem box, cent, cbounds, nvalid_buf, keys, keys_alt, vals, vals_alt, sort_tmp, leaf_parent, visit, gbox;
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
@@ -151,7 +151,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     const size_t N = (size_t)n;
     HIPCHK(c, c->box.ensure(N * 6 * sizeof(float)));
     HIPCHK(c, c->cent.ensure(N * 3 * sizeof(float)));
-    HIPCHK(c, c->cbounds.ensure(6 * sizeof(unsigned int)));
+    HIPCHK(c, c->cbounds.ensure(12 * sizeof(unsigned int)));
     HIPCHK(c, c->nvalid_buf.ensure(sizeof(unsigned int)));
     HIPCHK(c, c->keys.ensure(N * sizeof(unsigned long long)));
     HIPCHK(c, c->keys_alt.ensure(N * sizeof(unsigned long long)));
@@ -189,6 +189,15 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = nvalid;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
+    if (c->kernel == 0 && c->beam_key == 1) {
+        // tree order by (start, end): group boxes from the centroid order, then the second sort
+        HIPCHK(c, c->gbox.ensure(N * 6 * sizeof(float)));
+        b.gbox = c->gbox.as<float>();
+        HIPCHK(c, launch_tree_key(b, nvalid, c->stream));
+        HIPCHK(c, launch_sort(b, c->stream));
+    } else {
+        b.beam_key = 0;
+    }
     // kernel 0 runs the tile kernel on one tree of leaf2-beam tiles; kernels 2 / 4 / 5 on a tree of
     // BRE_OPT_LEAF_SIZE-beam leaves
     const int K = c->kernel == 0 ? c->leaf2 : c->leaf_size;
@@ -553,7 +562,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
                      &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index,
-                     &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf};
+                     &c->gbox, &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
@@ -630,7 +639,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->occupancy = (int)value;
         return BRE_OK;
     case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
-    case 110: c->beam_key = value == 1 ? 1 : 0; return BRE_OK;  // internal: beam sort key (study)
+    case 110: c->beam_key = value == 1 ? 1 : 0; return BRE_OK;  // internal: tree order (1 default, 0 centroid)
     case 109:  // internal: tile kernel partial-sum bytes per launch, in MiB (tests force several launches)
         if (value < 1 || value > ((int64_t)1 << 20)) return fail(c, BRE_ERR_INVALID_ARG, "partial cap must be in 1..2^20 MiB");
         c->partial_cap = value << 20;
@@ -839,7 +848,8 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     const uint64_t seq0 = (uint64_t)iteration * (uint64_t)n_photons + 1;
     const DevScene *ds = c->ph_scene.as<DevScene>();
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(c, launch_photons(ds, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(), nullptr,
+    const int sdepth = c->sc_head.stack_depth;
+    HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(), nullptr,
                              nullptr, nullptr, nullptr, nullptr, false, c->stream));
     HIPCHK(c, launch_count_scan(c->ph_tmp.ptr, c->ph_tmp.cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
                                 n_photons, c->stream));
@@ -853,7 +863,7 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
         HIPCHK(c, c->in_end.ensure(B * 3 * sizeof(float)));
         HIPCHK(c, c->in_radius.ensure(B * sizeof(float)));
         HIPCHK(c, c->in_power.ensure(B * 3 * sizeof(float)));
-        HIPCHK(c, launch_photons(ds, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
+        HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
                                  c->ph_offsets.as<int64_t>(), c->in_start.as<float>(), c->in_end.as<float>(),
                                  c->in_radius.as<float>(), c->in_power.as<float>(), true, c->stream));
     }
@@ -946,7 +956,8 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     CamSlots cs{c->cs_o.as<float>(), c->cs_p.as<float>(), c->cs_d.as<float>(), c->cs_t.as<float>(),
                 c->cs_pix.as<int32_t>(), c->cs_valid.as<int32_t>()};
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->cam_dev.as<DevCamera>(), c->cam_perms.as<uint16_t>(),
+    HIPCHK(c, launch_camera(c->ph_scene.as<DevScene>(), c->sc_head.stack_depth, c->cam_dev.as<DevCamera>(),
+                            c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
                             c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count,
                             c->shard_mode == 1 ? 0 : c->shard_block, c->stream));

@@ -13,10 +13,13 @@
 // giving every beam the union box of its equal-centroid group.
 //
 // Passes (all on the context stream):
-//   k_prep      per beam: WorldBound box (reference arithmetic), centroid, validity, centroid bounds
+//   k_prep      per beam: WorldBound box (reference arithmetic), centroid, validity, centroid and
+//               end-point bounds
 //   k_morton    per beam: 63-bit Morton key of the centroid (invalid beams sort last)
 //   radix sort  rocPRIM radix_sort_pairs (key, beam index)
-//   k_pack      per sorted beam: equal-centroid group box, 64-B BeamRec, scaled power
+//   k_group     (tree key 1) per beam: its equal-centroid group box, found in centroid order
+//   k_morton_se (tree key 1) per beam: 60-bit Morton key of (start, end), sorted again: the tree order
+//   k_pack      per sorted beam: (group) box, 64-B BeamRec, scaled power
 //   k_karras    per interior node: Karras 2012 split over leaf clusters of `leaf_size` beams
 //   k_refit     per leaf cluster: bottom-up union of child boxes (agent-scope release/acquire
 //               hand-off through one counter per node, cdna_hip_programming.md Guideline 16)
@@ -58,10 +61,12 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
                                                  const float *__restrict__ radius, int64_t n, int sqrt_mode,
                                                  float *__restrict__ box, float *__restrict__ cent,
                                                  unsigned int *__restrict__ cbounds, unsigned int *__restrict__ nvalid) {
-    __shared__ unsigned int red[kBlock / 64][7];
-    // ordered-uint min (lo) / max (hi) of valid centroids; identity values
+    __shared__ unsigned int red[kBlock / 64][13];
+    // ordered-uint min (lo) / max (hi) of valid centroids and of valid beams' end points; identity values
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
     unsigned int mx[3] = {0u, 0u, 0u};
+    unsigned int emn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
+    unsigned int emx[3] = {0u, 0u, 0u};
     unsigned int cnt = 0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         const f3 s = mk(start[3 * i], start[3 * i + 1], start[3 * i + 2]);
@@ -79,10 +84,14 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
         const bool valid = finite6(b) && isfinite(c.x) && isfinite(c.y) && isfinite(c.z);
         if (valid) {
             const unsigned int u[3] = {f2ord(c.x), f2ord(c.y), f2ord(c.z)};
+            const unsigned int us[3] = {f2ord(s.x), f2ord(s.y), f2ord(s.z)};
+            const unsigned int ue[3] = {f2ord(e.x), f2ord(e.y), f2ord(e.z)};
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 mn[k] = min(mn[k], u[k]);
                 mx[k] = max(mx[k], u[k]);
+                emn[k] = min(emn[k], min(us[k], ue[k]));
+                emx[k] = max(emx[k], max(us[k], ue[k]));
             }
             ++cnt;
         }
@@ -94,6 +103,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
         for (int k = 0; k < 3; ++k) {
             mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], off));
             mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
+            emn[k] = min(emn[k], (unsigned int)__shfl_xor((int)emn[k], off));
+            emx[k] = max(emx[k], (unsigned int)__shfl_xor((int)emx[k], off));
         }
         cnt += (unsigned int)__shfl_xor((int)cnt, off);
     }
@@ -103,6 +114,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
         for (int k = 0; k < 3; ++k) {
             red[w][k] = mn[k];
             red[w][3 + k] = mx[k];
+            red[w][7 + k] = emn[k];
+            red[w][10 + k] = emx[k];
         }
         red[w][6] = cnt;
     }
@@ -113,6 +126,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
             for (int k = 0; k < 3; ++k) {
                 mn[k] = min(mn[k], red[v][k]);
                 mx[k] = max(mx[k], red[v][3 + k]);
+                emn[k] = min(emn[k], red[v][7 + k]);
+                emx[k] = max(emx[k], red[v][10 + k]);
             }
             cnt += red[v][6];
         }
@@ -122,6 +137,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
             for (int k = 0; k < 3; ++k) {
                 atomicMin(&cbounds[k], mn[k]);
                 atomicMax(&cbounds[3 + k], mx[k]);
+                atomicMin(&cbounds[6 + k], emn[k]);
+                atomicMax(&cbounds[9 + k], emx[k]);
             }
         }
     }
@@ -163,10 +180,13 @@ __global__ __launch_bounds__(kBlock) void k_morton(const float *__restrict__ box
     vals[i] = (int32_t)i;
 }
 
-// Experimental beam key (BuildBuffers::beam_key 1): a 60-bit Morton key of the beam's start AND end
-// point (10 bits each, in the centroid box, clamped), so a leaf tile holds beams with both ends close
-// (a coherent line bundle) instead of beams with close centroids and any direction.  Speed study only:
-// the equal-centroid group boxes of k_pack are only found inside equal-key runs.
+// Tree order (BuildBuffers::beam_key 1, the default): a 60-bit Morton key of the beam's start AND
+// end point (10 bits each, in the box of all valid beams' end points), so a leaf tile holds beams
+// with both ends close -- a coherent bundle of nearly parallel, nearly coincident segments -- instead
+// of beams with close centroids and any direction (beam_key 0).  Tiles and the nodes above them are
+// then tighter (C2: 4858 -> 3596 beam lines staged per packet wave, 37% -> 45% of them kept by the
+// packet rejects, 2.67M -> 3.17M estimates/s, profiles/r3).  Only the tree's shape changes: every
+// beam is still tested with its own (group) box.
 __device__ __forceinline__ unsigned int q10(float x, float lo, float ext) {
     float u = ext > 0.0f ? (x - lo) / ext : 0.0f;
     u = fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
@@ -174,7 +194,7 @@ __device__ __forceinline__ unsigned int q10(float x, float lo, float ext) {
 }
 __global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ box, const float *__restrict__ cent,
                                                       const float *__restrict__ start, const float *__restrict__ end,
-                                                      const unsigned int *__restrict__ cbounds, int64_t n,
+                                                      const unsigned int *__restrict__ ebounds, int64_t n,
                                                       unsigned long long *__restrict__ keys,
                                                       int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -188,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ 
         unsigned int q[6];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const float lo = ord2f(cbounds[k]), hi = ord2f(cbounds[3 + k]);
+            const float lo = ord2f(ebounds[k]), hi = ord2f(ebounds[3 + k]);
             q[k] = q10(start[3 * i + k], lo, hi - lo);
             q[3 + k] = q10(end[3 * i + k], lo, hi - lo);
         }
@@ -202,12 +222,14 @@ __global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ 
     vals[i] = (int32_t)i;
 }
 
-__global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start, const float *__restrict__ end,
-                                                 const float *__restrict__ radius, const float *__restrict__ power,
-                                                 const float *__restrict__ box, const float *__restrict__ cent,
-                                                 const unsigned long long *__restrict__ keys,
-                                                 const int32_t *__restrict__ vals, int64_t nvalid,
-                                                 BeamRec *__restrict__ recs, float4 *__restrict__ pw) {
+// Equal-centroid groups in centroid-Morton order (the reference's multi-beam SAH leaves,
+// photonbeambvh.cpp:289-297): every valid beam's group box (the union of the boxes of the beams with
+// a bit-identical centroid; members share the centroid key, so they lie in one equal-key run),
+// written in input order for k_pack.
+__global__ __launch_bounds__(kBlock) void k_group(const float *__restrict__ box, const float *__restrict__ cent,
+                                                  const unsigned long long *__restrict__ keys,
+                                                  const int32_t *__restrict__ vals, int64_t nvalid,
+                                                  float *__restrict__ gbox) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= nvalid) return;
     const int32_t i = vals[s];
@@ -215,9 +237,43 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
     float lo[3] = {box[6 * i], box[6 * i + 1], box[6 * i + 2]};
     float hi[3] = {box[6 * i + 3], box[6 * i + 4], box[6 * i + 5]};
     const float c0 = cent[3 * i], c1 = cent[3 * i + 1], c2 = cent[3 * i + 2];
-    // Equal-centroid group (the reference's multi-beam SAH leaf): union of the members' boxes.
-    // Members share the Morton key, so they are within this key run.
-    for (int64_t t = s - 1; t >= 0 && keys[t] == key; --t) {
+    for (int dir = -1; dir <= 1; dir += 2) {
+        for (int64_t t = s + dir; t >= 0 && t < nvalid && keys[t] == key; t += dir) {
+            const int32_t j = vals[t];
+            if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = smin(lo[k], box[6 * j + k]);
+                    hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        gbox[6 * i + k] = lo[k];
+        gbox[6 * i + 3 + k] = hi[k];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start, const float *__restrict__ end,
+                                                 const float *__restrict__ radius, const float *__restrict__ power,
+                                                 const float *__restrict__ box, const float *__restrict__ cent,
+                                                 const unsigned long long *__restrict__ keys,
+                                                 const int32_t *__restrict__ vals, int64_t nvalid,
+                                                 const float *__restrict__ gbox, BeamRec *__restrict__ recs,
+                                                 float4 *__restrict__ pw) {
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= nvalid) return;
+    const int32_t i = vals[s];
+    const unsigned long long key = keys[s];
+    const float *bx = gbox ? gbox : box;  // gbox: the group boxes of k_group (tree key 1)
+    float lo[3] = {bx[6 * i], bx[6 * i + 1], bx[6 * i + 2]};
+    float hi[3] = {bx[6 * i + 3], bx[6 * i + 4], bx[6 * i + 5]};
+    const float c0 = cent[3 * i], c1 = cent[3 * i + 1], c2 = cent[3 * i + 2];
+    // Tree key 0: the equal-centroid group (the reference's multi-beam SAH leaf), the union of the
+    // members' boxes; members share the centroid key, so they are within this key run.
+    for (int64_t t = s - 1; !gbox && t >= 0 && keys[t] == key; --t) {
         const int32_t j = vals[t];
         if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
 #pragma unroll
@@ -227,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
             }
         }
     }
-    for (int64_t t = s + 1; t < nvalid && keys[t] == key; ++t) {
+    for (int64_t t = s + 1; !gbox && t < nvalid && keys[t] == key; ++t) {
         const int32_t j = vals[t];
         if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
 #pragma unroll
@@ -386,10 +442,14 @@ inline unsigned int grid_for(int64_t n) { return (unsigned int)((n + kBlock - 1)
 }  // namespace
 
 hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
-    // cbounds: min = 0xffffffff, max = 0; nvalid = 0
+    // cbounds: centroid min = 0xffffffff, max = 0, then end-point min / max; nvalid = 0
     hipError_t e = hipMemsetAsync(b.cbounds, 0xff, 3 * sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(b.cbounds + 3, 0, 3 * sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.cbounds + 6, 0xff, 3 * sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.cbounds + 9, 0, 3 * sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(b.nvalid, 0, sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
@@ -402,12 +462,18 @@ hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
 
 hipError_t launch_morton(const BuildBuffers &b, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
-    if (b.beam_key == 1 && b.start && b.end)
-        hipLaunchKernelGGL(k_morton_se, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.start, b.end,
-                           b.cbounds, b.n, b.keys, b.vals);
-    else
-        hipLaunchKernelGGL(k_morton, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.cbounds, b.n, b.keys,
-                           b.vals);
+    hipLaunchKernelGGL(k_morton, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.cbounds, b.n, b.keys,
+                       b.vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
+    if (b.n == 0) return hipSuccess;
+    if (nvalid > 0)
+        hipLaunchKernelGGL(k_group, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.box, b.cent, b.keys_alt, b.vals_alt,
+                           nvalid, b.gbox);
+    hipLaunchKernelGGL(k_morton_se, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.start, b.end,
+                       b.cbounds + 6, b.n, b.keys, b.vals);
     return hipGetLastError();
 }
 
@@ -429,7 +495,7 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s) {
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (nvalid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power, b.box,
-                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.recs, b.pow);
+                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key == 1 ? b.gbox : nullptr, b.recs, b.pow);
     return hipGetLastError();
 }
 

@@ -526,13 +526,14 @@ int64_t camera_slots(int width, int height) {
     return (int64_t)((width + 7) / 8) * ((height + 7) / 8) * 64;
 }
 
-hipError_t launch_camera(const DevScene *scene, const DevCamera *cam, const uint16_t *perms, int width, int height,
-                         int iteration, int max_depth, int render_surfaces, int render_media, const CamSlots &s,
-                         float *surface, unsigned int *flags, int shard_rank, int shard_count, int shard_block,
-                         hipStream_t stream) {
+hipError_t launch_camera(const DevScene *scene, int stack_depth, const DevCamera *cam, const uint16_t *perms, int width,
+                         int height, int iteration, int max_depth, int render_surfaces, int render_media,
+                         const CamSlots &s, float *surface, unsigned int *flags, int shard_rank, int shard_count,
+                         int shard_block, hipStream_t stream) {
     const int64_t nslots = camera_slots(width, height);
     if (nslots == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_camera, dim3((unsigned)(nslots / kCamBlock)), dim3(kCamBlock), 0, stream, scene, cam, perms,
+    hipLaunchKernelGGL(k_camera, dim3((unsigned)(nslots / kCamBlock)), dim3(kCamBlock),
+                       scene_stack_bytes(stack_depth, kCamBlock), stream, scene, cam, perms,
                        iteration, max_depth, render_surfaces, render_media, nslots, s.o, s.p, s.d, s.t, s.pix,
                        s.valid, surface, flags, shard_rank, shard_count, shard_block);
     return hipGetLastError();

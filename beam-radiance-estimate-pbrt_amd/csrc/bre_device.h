@@ -63,11 +63,12 @@ struct BuildBuffers {
     int64_t n;
     int sqrt_mode;
     int leaf_size;
-    int beam_key = 0;  // 0: Morton of the box centroid; 1 (study): Morton of (start, end)
+    int beam_key = 1;  // tree order: 1 Morton of (start, end) (default), 0 Morton of the box centroid
     // scratch
     float *box;        // 6n (input order)
     float *cent;       // 3n (input order)
-    unsigned int *cbounds;  // 6 ordered-uint min/max of valid centroids
+    unsigned int *cbounds;  // 12 ordered uints: min/max of valid centroids, then of their end points
+    float *gbox;            // 6n (input order): equal-centroid group boxes (tree key 1)
     unsigned int *nvalid;   // 1
     unsigned long long *keys, *keys_alt;
     int32_t *vals, *vals_alt;
@@ -102,6 +103,8 @@ hipError_t launch_morton(const BuildBuffers &b, hipStream_t s);
 size_t sort_temp_bytes(int64_t n);
 hipError_t launch_sort(const BuildBuffers &b, hipStream_t s);
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
+// tree key 1, after the centroid sort: group boxes (k_group), then the (start, end) keys into keys/vals
+hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 
 // One gathered segment as the tile kernel's exact stage reads it (k_seg_prep): 64 B as four 16-B

@@ -103,6 +103,7 @@ void prepare_geometry(const bre_scene *s, HostScene *out) {
     }
     out->depth = build_scene_bvh(out->tris, &out->nodes, &out->prims);
     d.n_nodes = (int)out->nodes.size();
+    d.stack_depth = out->depth;
 }
 
 void prepare_scene(const bre_scene *s, HostScene *out, const float *d_density) {
@@ -288,15 +289,16 @@ inline unsigned grid_of(int64_t n) { return (unsigned)((n + kPhotonBlock - 1) / 
 
 }  // namespace
 
-hipError_t launch_photons(const DevScene *scene, int64_t n, uint64_t seq0, int max_depth, float radius,
-                          int32_t *counts, const int64_t *offsets, float *start, float *end, float *rad,
-                          float *power, bool emit, hipStream_t s) {
+hipError_t launch_photons(const DevScene *scene, int stack_depth, int64_t n, uint64_t seq0, int max_depth,
+                          float radius, int32_t *counts, const int64_t *offsets, float *start, float *end,
+                          float *rad, float *power, bool emit, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    const size_t lds = scene_stack_bytes(stack_depth, kPhotonBlock);
     if (emit)
-        hipLaunchKernelGGL(k_photons<true>, dim3(grid_of(n)), dim3(kPhotonBlock), 0, s, scene, n, seq0, max_depth,
+        hipLaunchKernelGGL(k_photons<true>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
                            radius, counts, offsets, start, end, rad, power);
     else
-        hipLaunchKernelGGL(k_photons<false>, dim3(grid_of(n)), dim3(kPhotonBlock), 0, s, scene, n, seq0, max_depth,
+        hipLaunchKernelGGL(k_photons<false>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
                            radius, counts, offsets, start, end, rad, power);
     return hipGetLastError();
 }

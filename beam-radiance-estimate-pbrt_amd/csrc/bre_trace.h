@@ -163,10 +163,11 @@ struct SceneNode {
     uint8_t pad;
 };
 static_assert(sizeof(SceneNode) == 32, "SceneNode is BVHAccel's 32-B LinearBVHNode");
-constexpr int kSceneStack = 64;  // BVHAccel::Intersect's nodesToVisit[64]
+constexpr int kSceneStack = 64;  // BVHAccel::Intersect's nodesToVisit[64]: the deepest tree accepted
 
 struct DevScene {
     int n_tris, n_lights, medium, n_nodes;  // medium: BRE_MEDIUM_NONE / _HOMOGENEOUS / _GRID
+    int stack_depth;                        // traversal stack entries per thread (the tree depth)
     float sigma_t[3];
     float g;
     // the triangles in scene order, the BVHAccel over them (nodes + primitive order) and
@@ -286,11 +287,15 @@ __device__ __forceinline__ bool intersect_tri(const PTri &T, f3 o, f3 dir, float
 // first by dirIsNeg[axis], every node tested with the reference's slab test against the CURRENT
 // tMax, every leaf triangle with Triangle::Intersect, each hit shrinking tMax (primitive.cpp:97-101).
 // The triangles are tested in the reference's order, so among equal-t hits the same one wins.  The
-// host checks the tree depth against kSceneStack (prepare_scene), so the stack cannot overflow.
+// stack lives in the kernel's dynamic LDS (entry k of thread t at [k * blockDim.x + t]), sized by
+// the launch to the tree's depth (scene_stack_bytes): it holds at most one entry per level of the
+// current path.  The host rejects trees deeper than kSceneStack (upload_scene).
 __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, float &tmax, Hit &h) {
+    extern __shared__ int bre_scene_stack[];
+    int *stack = bre_scene_stack + threadIdx.x;
+    const int stride = blockDim.x;
     const f3 inv = mk(1 / d.x, 1 / d.y, 1 / d.z);
     const int n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
-    int stack[kSceneStack];
     int sp = 0, cur = 0;
     bool hit = false;
     while (true) {
@@ -310,20 +315,15 @@ __device__ __forceinline__ bool intersect_scene(const DevScene &S, f3 o, f3 d, f
                     hit = true;
                 }
                 if (sp == 0) break;
-                cur = stack[--sp];
+                cur = stack[--sp * stride];
             } else {
                 const int neg = nd.axis == 0 ? n0 : (nd.axis == 1 ? n1 : n2);
-                if (neg) {
-                    stack[sp++] = cur + 1;
-                    cur = nd.offset;
-                } else {
-                    stack[sp++] = nd.offset;
-                    cur = cur + 1;
-                }
+                stack[sp++ * stride] = neg ? cur + 1 : nd.offset;
+                cur = neg ? nd.offset : cur + 1;
             }
         } else {
             if (sp == 0) break;
-            cur = stack[--sp];
+            cur = stack[--sp * stride];
         }
     }
     return hit;
@@ -552,19 +552,25 @@ struct CamSlots {
 
 void prepare_camera(const bre_scene *s, int width, int height, DevCamera *c, std::vector<uint16_t> *perms);
 int64_t camera_slots(int width, int height);
-hipError_t launch_camera(const DevScene *scene, const DevCamera *cam, const uint16_t *perms, int width, int height,
-                         int iteration, int max_depth, int render_surfaces, int render_media, const CamSlots &s,
-                         float *surface, unsigned int *flags, int shard_rank, int shard_count, int shard_block, hipStream_t stream);
+hipError_t launch_camera(const DevScene *scene, int stack_depth, const DevCamera *cam, const uint16_t *perms, int width,
+                         int height, int iteration, int max_depth, int render_surfaces, int render_media,
+                         const CamSlots &s, float *surface, unsigned int *flags, int shard_rank, int shard_count,
+                         int shard_block, hipStream_t stream);
 size_t camera_scan_temp_bytes(int64_t n);
 hipError_t launch_camera_scan(void *tmp, size_t tmp_bytes, const CamSlots &s, int64_t nslots, int max_depth,
                               int64_t *offs, hipStream_t stream);
 hipError_t launch_camera_compact(const CamSlots &s, int64_t nslots, int max_depth, const int64_t *offs, float *o,
                                  float *p, float *d, float *t, int32_t *pix, int32_t *depth, hipStream_t stream);
 
+// dynamic LDS of a photon / camera launch: the scene traversal stack of every thread of a block
+inline size_t scene_stack_bytes(int stack_depth, int block) {
+    return (size_t)(stack_depth > 0 ? stack_depth : 1) * (size_t)block * sizeof(int);
+}
+
 // photon pass launchers (bre_photon.hip)
-hipError_t launch_photons(const DevScene *scene, int64_t n, uint64_t seq0, int max_depth, float radius,
-                          int32_t *counts, const int64_t *offsets, float *start, float *end, float *rad,
-                          float *power, bool emit, hipStream_t s);
+hipError_t launch_photons(const DevScene *scene, int stack_depth, int64_t n, uint64_t seq0, int max_depth,
+                          float radius, int32_t *counts, const int64_t *offsets, float *start, float *end,
+                          float *rad, float *power, bool emit, hipStream_t s);
 size_t count_scan_temp_bytes(int64_t n);
 hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n,
                              hipStream_t s);

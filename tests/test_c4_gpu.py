@@ -42,9 +42,14 @@ def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
     it = 0
     R = bre.beam_radius_at(0.01, 0.5, it)
     t0 = time.perf_counter()
+
+    def progress(msg):  # a line per phase (long GPU phases: a run that prints nothing looks hung)
+        print(f"C4 [{time.perf_counter() - t0:6.1f} s] {msg}", flush=True)
+
     with bre.BeamGather(0) as g:  # kernel 0, counters off, sort on: the bench configuration
         nb = g.trace_photons(scene, PHOTONS, it, 5, R)
         n = g.camera_pass(scene, W, H, it, 5, True, True)
+        progress(f"photon pass {nb} beams, camera pass {n} segments")
         seg_rgb = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
         counts = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
         ld1 = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
@@ -52,6 +57,7 @@ def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
         g.gather_camera_segments(R, accum=ld1, seg_rgb=seg_rgb, counts=counts)
         g.synchronize()
         t2 = time.perf_counter()
+        progress("full gather done")
         # (b) the 8 packet shards of this iteration, one after another on this GPU
         films = []
         for rank in range(WORLD):
@@ -60,6 +66,7 @@ def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
             g.gather_camera(R, f)
             g.synchronize()
             films.append(f)
+            progress(f"packet shard {rank} of {WORLD} done")
         t3 = time.perf_counter()
         g.set_shard(0, 1, 1, packets=True)
         beams = g.get_beams()
@@ -84,6 +91,7 @@ def test_c4_full_size_production_and_packet_shards(bre, oracle, scene_mod_gpu):
     idx = np.random.default_rng(4000).choice(n, NSAMPLE, replace=False)
     sample = {k: np.ascontiguousarray(segs[k][idx]) for k in ("o", "p", "d", "tmax")}
     t4 = time.perf_counter()
+    progress("oracle on the sampled segments")
     ref = oracle.bruteforce(beams, sample, R, nthreads=16)
     print(f"C4 oracle: {NSAMPLE} segments x {nb} beams in {time.perf_counter() - t4:.1f} s, "
           f"{int(ref['contrib'].sum())} contributions")
