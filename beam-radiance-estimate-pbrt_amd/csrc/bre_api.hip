@@ -64,13 +64,13 @@ struct bre_ctx {
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
     int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
-    int sort_key = 1;        // segment coherence sort key (SegSort::key_mode; 1 measured best at C2)
+    int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
     int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
-    int beam_key = 1;        // internal: tree order of the build (BuildBuffers::beam_key): 1 (start, end), 0 centroid
+    int beam_key = 2;        // internal: tree order of the build (BuildBuffers::beam_key): 2 / 1 (start, end) Hilbert / Morton, 0 centroid
     int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -189,7 +189,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nvalid = nvalid;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
-    if (c->kernel == 0 && c->beam_key == 1) {
+    if (c->kernel == 0 && c->beam_key >= 1) {
         // tree order by (start, end): group boxes from the centroid order, then the second sort
         HIPCHK(c, c->gbox.ensure(N * 6 * sizeof(float)));
         b.gbox = c->gbox.as<float>();
@@ -638,8 +638,14 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
             return fail(c, BRE_ERR_INVALID_ARG, "occupancy must be 1 or 4..8");
         c->occupancy = (int)value;
         return BRE_OK;
-    case 105: c->sort_key = (int)value; return BRE_OK;  // internal: segment sort key (sweeps)
-    case 110: c->beam_key = value == 1 ? 1 : 0; return BRE_OK;  // internal: tree order (1 default, 0 centroid)
+    case 105:  // internal: segment sort key (SegSort::key_mode, sweeps)
+        if (value < 0 || value > 4) return fail(c, BRE_ERR_INVALID_ARG, "segment sort key must be 0..4");
+        c->sort_key = (int)value;
+        return BRE_OK;
+    case 110:  // internal: tree order (1 (start, end) Morton, default; 2 the same in Hilbert order; 0 centroid)
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "tree order must be 0..2");
+        c->beam_key = (int)value;
+        return BRE_OK;
     case 109:  // internal: tile kernel partial-sum bytes per launch, in MiB (tests force several launches)
         if (value < 1 || value > ((int64_t)1 << 20)) return fail(c, BRE_ERR_INVALID_ARG, "partial cap must be in 1..2^20 MiB");
         c->partial_cap = value << 20;

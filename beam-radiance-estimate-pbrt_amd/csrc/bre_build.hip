@@ -180,13 +180,16 @@ __global__ __launch_bounds__(kBlock) void k_morton(const float *__restrict__ box
     vals[i] = (int32_t)i;
 }
 
-// Tree order (BuildBuffers::beam_key 1, the default): a 60-bit Morton key of the beam's start AND
+// Tree order (BuildBuffers::beam_key 1 and 2): a 60-bit key of the beam's start AND
 // end point (10 bits each, in the box of all valid beams' end points), so a leaf tile holds beams
 // with both ends close -- a coherent bundle of nearly parallel, nearly coincident segments -- instead
 // of beams with close centroids and any direction (beam_key 0).  Tiles and the nodes above them are
 // then tighter (C2: 4858 -> 3596 beam lines staged per packet wave, 37% -> 45% of them kept by the
 // packet rejects, 2.67M -> 3.17M estimates/s, profiles/r3).  Only the tree's shape changes: every
-// beam is still tested with its own (group) box.
+// beam is still tested with its own (group) box.  beam_key 2 (the default) orders the same six
+// 10-bit coordinates along a Hilbert curve instead of a Morton curve: consecutive keys never jump
+// across the box, so fewer tiles straddle two distant bundles (C2 +2.2%, and +6.4% together with the
+// Hilbert segment order, profiles/r3/sweep2).
 __device__ __forceinline__ unsigned int q10(float x, float lo, float ext) {
     float u = ext > 0.0f ? (x - lo) / ext : 0.0f;
     u = fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
@@ -195,7 +198,7 @@ __device__ __forceinline__ unsigned int q10(float x, float lo, float ext) {
 __global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ box, const float *__restrict__ cent,
                                                       const float *__restrict__ start, const float *__restrict__ end,
                                                       const unsigned int *__restrict__ ebounds, int64_t n,
-                                                      unsigned long long *__restrict__ keys,
+                                                      int hilbert, unsigned long long *__restrict__ keys,
                                                       int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -212,11 +215,15 @@ __global__ __launch_bounds__(kBlock) void k_morton_se(const float *__restrict__ 
             q[k] = q10(start[3 * i + k], lo, hi - lo);
             q[3 + k] = q10(end[3 * i + k], lo, hi - lo);
         }
-        key = 0ull;
+        if (hilbert) {
+            key = hilbert_key<6, 10>(q);
+        } else {
+            key = 0ull;
 #pragma unroll
-        for (int bit = 9; bit >= 0; --bit)
+            for (int bit = 9; bit >= 0; --bit)
 #pragma unroll
-            for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+                for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+        }
     }
     keys[i] = key;
     vals[i] = (int32_t)i;
@@ -473,7 +480,7 @@ hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s)
         hipLaunchKernelGGL(k_group, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.box, b.cent, b.keys_alt, b.vals_alt,
                            nvalid, b.gbox);
     hipLaunchKernelGGL(k_morton_se, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.start, b.end,
-                       b.cbounds + 6, b.n, b.keys, b.vals);
+                       b.cbounds + 6, b.n, b.beam_key == 2 ? 1 : 0, b.keys, b.vals);
     return hipGetLastError();
 }
 
@@ -495,7 +502,7 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s) {
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (nvalid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power, b.box,
-                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key == 1 ? b.gbox : nullptr, b.recs, b.pow);
+                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key >= 1 ? b.gbox : nullptr, b.recs, b.pow);
     return hipGetLastError();
 }
 

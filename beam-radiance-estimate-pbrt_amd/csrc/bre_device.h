@@ -63,7 +63,7 @@ struct BuildBuffers {
     int64_t n;
     int sqrt_mode;
     int leaf_size;
-    int beam_key = 1;  // tree order: 1 Morton of (start, end) (default), 0 Morton of the box centroid
+    int beam_key = 2;  // tree order: 2 Hilbert of (start, end) (default), 1 Morton of (start, end), 0 Morton of the centroid
     // scratch
     float *box;        // 6n (input order)
     float *cent;       // 3n (input order)
@@ -213,7 +213,8 @@ struct SegSort {
     float *o2, *p2, *d2, *t2;  // sorted copies
     int32_t *pix2;
     int key_mode;  // 0: Morton of (origin, octahedral direction); 1: Morton of (origin, end point);
-                   // 2 / 3: the segment's line (dominant-axis class + slopes + plane crossing [+ midpoint])
+                   // 2 / 3: the segment's line (dominant-axis class + slopes + plane crossing [+ midpoint]);
+                   // 4: Hilbert order of (origin, end point) (the default, bre_math.h hilbert_key)
 };
 size_t seg_sort_temp_bytes(int64_t n);
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);

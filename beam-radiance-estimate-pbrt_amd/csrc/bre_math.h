@@ -187,4 +187,38 @@ __host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, f
     return closest_distance_t<false>(a0, a1, au, mag_a, b0, bu, mag_b, dist, unused);
 }
 
+// Hilbert curve index of an n-dimensional point with b bits per coordinate (Skilling, "Programming
+// the Hilbert curve", AIP Conf. Proc. 707, 2004: AxestoTranspose, then the bits interleaved from the
+// most significant down).  A Hilbert order has no long jumps between consecutive cells, unlike a
+// Morton order, so runs of consecutive keys (leaf tiles, segment packets) are more compact.
+template <int N, int B>
+__host__ __device__ __forceinline__ unsigned long long hilbert_key(unsigned int x[N]) {
+    const unsigned int M = 1u << (B - 1);
+    for (unsigned int Q = M; Q > 1; Q >>= 1) {  // inverse undo
+        const unsigned int P = Q - 1;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (x[i] & Q) {
+                x[0] ^= P;  // invert
+            } else {        // exchange
+                const unsigned int t = (x[0] ^ x[i]) & P;
+                x[0] ^= t;
+                x[i] ^= t;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 1; i < N; ++i) x[i] ^= x[i - 1];  // Gray encode
+    unsigned int t = 0;
+    for (unsigned int Q = M; Q > 1; Q >>= 1)
+        if (x[N - 1] & Q) t ^= Q - 1;
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] ^= t;
+    unsigned long long key = 0ull;
+    for (int bit = B - 1; bit >= 0; --bit)
+#pragma unroll
+        for (int i = 0; i < N; ++i) key = (key << 1) | ((x[i] >> bit) & 1u);
+    return key;
+}
+
 }  // namespace bre

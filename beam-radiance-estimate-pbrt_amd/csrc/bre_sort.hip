@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_keys(int64_t n, const float *__r
 // 6-D Morton key: 10 bits each of origin x, y, z and end point x, y, z (in the box of both)
 __global__ __launch_bounds__(kBlock) void k_seg_keys_op(int64_t n, const float *__restrict__ o,
                                                         const float *__restrict__ p, const unsigned int *__restrict__ b,
-                                                        unsigned long long *__restrict__ keys,
+                                                        int hilbert, unsigned long long *__restrict__ keys,
                                                         int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -152,10 +152,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_keys_op(int64_t n, const float *
         q[3 + k] = quant10(ext > 0.f ? (p[3 * i + k] - lo[k]) / ext : 0.f);
     }
     unsigned long long key = 0ull;
+    if (hilbert) {
+        key = hilbert_key<6, 10>(q);
+    } else {
 #pragma unroll
-    for (int bit = 9; bit >= 0; --bit)
+        for (int bit = 9; bit >= 0; --bit)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+            for (int k = 0; k < 6; ++k) key = (key << 1) | ((q[k] >> bit) & 1u);
+    }
     keys[i] = key;
     vals[i] = (int32_t)i;
 }
@@ -308,10 +312,10 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     const unsigned bgrid = grid_of(s.n) < 1024u ? grid_of(s.n) : 1024u;  // grid-stride bounds
     hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
     int key_bits = 50;
-    if (s.key_mode == 1) {
+    if (s.key_mode == 1 || s.key_mode == 4) {
         hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.p, s.bounds);
-        hipLaunchKernelGGL(k_seg_keys_op, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.bounds, s.keys,
-                           s.vals);
+        hipLaunchKernelGGL(k_seg_keys_op, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.o, s.p, s.bounds,
+                           s.key_mode == 4 ? 1 : 0, s.keys, s.vals);
         key_bits = 60;
     } else if (s.key_mode == 2 || s.key_mode == 3) {
         hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.p, s.bounds);

@@ -474,3 +474,27 @@ def test_segment_repeated_through_whole_batches(bre, oracle):
     assert np.array_equal(out["counts"][:, 1], ref["contrib"])
     assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL
     assert np.array_equal(out["seg_rgb"], outs[0]["seg_rgb"])
+
+
+@pytest.mark.parametrize("beam_key", [0, 1, 2])
+def test_tree_and_segment_orders_give_exact_sets(bre, synth, oracle, beam_key):
+    """The tree order (option 110: centroid Morton 0, (start, end) Morton 1, (start, end) Hilbert 2 =
+    default) and the segment coherence-sort key (option 105: 0-4, Hilbert 4 = default) only reorder
+    work: every combination gives the oracle's exact contribution counts and its sums to rounding;
+    out-of-range keys are rejected."""
+    beams = synth.fog_beams(20000, seed=91)
+    segs = synth.bounce_segments(4096, seed=92)
+    ref = oracle.build(beams).gather(segs, 0.01)
+    assert ref["contrib"].sum() > 0
+    for sort_key in range(5):
+        with bre.BeamGather(0, counters=False, kernel=0) as g:
+            g.set_option(110, beam_key)
+            g.set_option(105, sort_key)
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            out = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=0.01, counts=True)
+        assert np.array_equal(out["counts"][:, 1], ref["contrib"]), sort_key
+        assert _seg_close(out["seg_rgb"], ref["seg_rgb"]) <= SEG_RTOL, sort_key
+    with bre.BeamGather(0) as g:
+        for opt, bad in ((110, 3), (110, -1), (105, 5)):
+            with pytest.raises(bre.BreError):
+                g.set_option(opt, bad)
