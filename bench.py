@@ -24,12 +24,15 @@ pixel bands.  `--scaling weak` gives every rank its own film of the same size (N
 `--emulate-shard R/N` runs rank R's share of an N-GPU strong-scaling run alone on one GPU.
 
 Also reported (rank 0, N = 1):
-* `roofline` — HBM: the tile kernel's algorithmic bytes per launch (what its packets must read: node
-  and beam lines of the visited tiles, the segments, the partial sums; counted live by the counter
-  pass) / its HIP-event launch time; `traffic` = HBM bytes per launch from this run's own rocprofv3
-  PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); `issue` = SQ counters of the same
-  passes (VALU issue and LDS utilisation: the kernel's real bound); the SURVEY §8d reference-tree
-  byte model is kept as `ref_model_*` (not a fraction: one staged beam line feeds 64 lanes).
+* `roofline` — the tile kernel's binding unit, VALU issue (`bound` "valu_issue"): wave64 VALU
+  instructions per second of the iteration-0 launch against 256 CU x 4 SIMD / 2 clocks, from this
+  run's own rocprofv3 PMC passes (`issue`: SQ counters, LDS busy, waits); `traffic` = HBM bytes per
+  launch from the same passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE).  `hbm`: the
+  algorithmic bytes per launch (node and beam lines of the visited tiles, the segments, the exact
+  stage's 144 B per queued pair, the partial sums; counted live by the counter pass) / the launch's
+  HIP-event time against 8 TB/s, and the measured HBM traffic against it.  Without rocprofv3 the
+  line falls back to `bound` "hbm" on the algorithmic bytes.  The SURVEY §8d reference-tree byte
+  model is kept as `ref_model_*` (not a fraction: one staged beam line feeds 64 lanes).
 * `cpu_baseline` — the oracle's CPU restatement of the reference algorithm (SAH tree, per-query
   vector<shared_ptr>, all host threads, plus 1 thread), timed on bounded samples of the same
   segments and beams at the first and last timed iterations.
@@ -346,7 +349,15 @@ def main():
 
 
 def roofline(st, args, wl, gather_ms, pmc, cpu):
-    """HBM roofline of the tile kernel for one launch of iteration 0 (see the module docstring)."""
+    """Roofline of the tile kernel for one launch of iteration 0 (see the module docstring).
+
+    The binding unit is VALU issue: `achieved` = the launch's wave64 VALU instructions
+    (SQ_INSTS_VALU) per second, `peak` = 256 CU x 4 SIMD x one wave64 instruction per 2 clocks at the
+    clock the same counters measured, so `frac` = the VALU issue fraction.  The byte side is kept in
+    `hbm`: the algorithmic bytes the packets request per launch against the 8 TB/s HBM peak (served
+    mostly from L1 / L2 / Infinity Cache: the requests exceed what HBM could deliver) and the HBM
+    traffic the FETCH/WRITE counters measure.  Without the PMC passes the line falls back to the HBM
+    roofline of the algorithmic bytes."""
     nseg = max(st["n_segments"], 1)
     items = (nseg + 63) // 64 * args.split
     # what the packet algorithm must read / write per launch: every visited node line and staged
@@ -357,25 +368,34 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     queued = st.get("queued_pairs", 0)
     alg = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + 144.0 * queued
            + nseg * 12 * (args.split + 1))
-    achieved = alg / (gather_ms * 1e-3) / 1e9
-    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-           "kernel": "k_gather_tile (+ k_reduce)", "launch": "iteration 0", "launch_ms": gather_ms,
+    requested = alg / (gather_ms * 1e-3) / 1e9
+    hbm = {"requested_GBps": requested, "peak": HBM_PEAK_GBPS, "requested_over_peak": requested / HBM_PEAK_GBPS,
            "algorithmic_bytes_per_launch": alg, "queued_pairs_per_launch": queued,
            "algorithmic_model": "64 B x (node visits + beam lines staged) + 52 B x 64 per (packet, subtree) "
                                 "item + 144 B per queued exact-stage pair + 12 B x (split + 1) per segment; "
                                 "counts from this run's counter pass"}
+    out = {"bound": "hbm", "achieved": requested, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": requested / HBM_PEAK_GBPS, "traffic": None,
+           "kernel": "k_gather_tile (+ k_reduce)", "launch": "iteration 0", "launch_ms": gather_ms}
     if pmc:
         out["traffic"] = pmc.get("traffic_bytes_per_launch")
         out["traffic_source"] = pmc.get("source")
         if out["traffic"]:
-            out["traffic_GBps"] = out["traffic"] / (pmc["kernel_ms"] * 1e-3) / 1e9
-            out["traffic_over_algorithmic"] = out["traffic"] / alg
-        if pmc.get("issue"):
-            out["issue"] = pmc["issue"]
-            # the unit that binds the kernel: VALU issue, not HBM bandwidth
-            out["binding_unit"] = "valu_issue"
-            out["bound_frac"] = pmc["issue"]["valu_issue_frac"]
+            hbm["traffic_bytes_per_launch"] = out["traffic"]
+            hbm["traffic_GBps"] = out["traffic"] / (pmc["kernel_ms"] * 1e-3) / 1e9
+            hbm["traffic_frac"] = hbm["traffic_GBps"] / HBM_PEAK_GBPS
+            hbm["traffic_over_algorithmic"] = out["traffic"] / alg
+        iss = pmc.get("issue")
+        if iss:
+            t = pmc["kernel_ms"] * 1e-3
+            clock_hz = iss["clocks"] / t
+            out.update({"bound": "valu_issue", "unit": "G wave64 VALU inst/s",
+                        "achieved": iss["SQ_INSTS_VALU"] / t / 1e9,
+                        "peak": CUS * SIMDS / 2.0 * clock_hz / 1e9,
+                        "frac": iss["valu_issue_frac"], "clock_GHz": clock_hz / 1e9,
+                        "pmc_launch_ms": pmc["kernel_ms"]})
+            out["issue"] = iss
+    out["hbm"] = hbm
     if cpu and cpu.get("visit_mean"):
         # SURVEY.md §8d's reference-tree model (every segment streams its candidates from HBM):
         # kept for comparison, not a fraction of HBM peak

@@ -23,6 +23,15 @@ def main(d, out):
         res[k]["calls"] = int(r["Calls"])
         res[k]["avg_ns"] = float(r["AverageNs"])
         res[k]["total_ns"] = float(r["TotalDurationNs"])
+    # per-dispatch durations of the gather kernels, in launch order (the bench's iteration-0 launch is
+    # the one its roofline times with HIP events)
+    trace = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        for r in csv.DictReader(open(trace)):
+            k = short(r["Kernel_Name"])
+            if "gather" in k and k in res:
+                ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+                res[k].setdefault("dispatch_ms", []).append(round(ms, 3))
     for cname, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):

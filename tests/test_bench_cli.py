@@ -31,13 +31,24 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
             return 1000
 
     a = bench.parse(["--split", "4"])
-    st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000}
+    st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000, "queued_pairs": 500}
     r = bench.roofline(st, a, WL(), 2.0, None, None)
     items = (640 + 63) // 64 * 4
-    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 640 * 12 * (4 + 1)
-    assert r["algorithmic_bytes_per_launch"] == alg
+    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 144.0 * 500 + 640 * 12 * (4 + 1)
+    # without the PMC passes: the HBM roofline of the algorithmic bytes
+    assert r["bound"] == "hbm" and r["hbm"]["algorithmic_bytes_per_launch"] == alg
     assert r["achieved"] == pytest.approx(alg / 2e-3 / 1e9)
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and r["unit"] == "GB/s" and r["traffic"] is None
+    # with them: VALU issue binds; frac = instructions / (256 CU x 4 SIMD / 2 x clocks), HBM kept aside
+    issue = {"SQ_INSTS_VALU": 3.0e9, "clocks": 2.0e7, "valu_issue_frac": 3.0e9 / (512 * 2.0e7)}
+    pmc = {"traffic_bytes_per_launch": 4.0e9, "kernel_ms": 10.0, "source": "test", "issue": issue}
+    r = bench.roofline(st, a, WL(), 2.0, pmc, None)
+    assert r["bound"] == "valu_issue" and r["traffic"] == 4.0e9
+    assert r["achieved"] == pytest.approx(3.0e9 / 1e-2 / 1e9)
+    assert r["peak"] == pytest.approx(512 * 2.0e7 / 1e-2 / 1e9)  # 2 GHz
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) == pytest.approx(issue["valu_issue_frac"])
+    assert r["hbm"]["traffic_GBps"] == pytest.approx(4.0e9 / 1e-2 / 1e9)
+    assert r["hbm"]["traffic_over_algorithmic"] == pytest.approx(4.0e9 / alg)
 
 
 def test_host_threads_positive(bench):
