@@ -63,6 +63,7 @@ struct bre_ctx {
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
+    int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
@@ -419,6 +420,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.occupancy = c->occupancy;
     a.block_map = c->block_map;
     a.tscan = c->tscan;
+    a.margin = c->margin;
     a.stack_cap = c->stack_cap;
     c->stats.n_segments = nseg;
     if (c->nvalid == 0) {
@@ -657,6 +659,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)
         if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
         c->tscan = (int)value;
+        return BRE_OK;
+    case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
+        c->margin = (int)value;
         return BRE_OK;
     default: return fail(c, BRE_ERR_INVALID_ARG, "unknown option %d", option);
     }

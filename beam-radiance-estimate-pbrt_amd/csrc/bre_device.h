@@ -152,6 +152,7 @@ struct GatherArgs {
     int stack_cap;         // traversal stack entries to use (0 = all); tests force an overflow
     int block_map;         // tile kernel block -> (packet, subtree) mapping (k_gather_tile)
     int tscan;             // tile kernel: transposed scan when on-lanes * 8 < kept beams * tscan (0: off)
+    int margin;            // tile kernel prefilter margins: 1 = the tight bound (default), 0 = round 2's
 };
 
 // capsule-chunk index (bre_chunk.hip)

@@ -262,9 +262,20 @@ __device__ __forceinline__ bool bundle_box_miss(const Bundle &K, const Box6 &b) 
     return (bsum == bsum) & (tn > tf);
 }
 
-// far_from_lines_fast's bound (bre_lane.h) for the bundle's line against a beam line, with
-// maxd + delta: a rejection proves that every lane's computed ComputeClosestPoints distance is >= maxd.
-__device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float maxd) {
+// Packet-level line reject of a beam: a rejection proves that every lane's computed
+// ComputeClosestPoints distance is >= maxd.  Every lane's segment lies within delta of the bundle
+// line C, so its distance from the beam LINE B is >= D(C, B) - delta.  The reference's pA lies on
+// the segment to within 10U Ma + U Ol (U = 2^-24; see the margin note above ScanLane), and its pB on
+// line B to within 2U |t1| + U Bl; a pair can only contribute if |pA - pB| < maxd, which puts pB
+// within maxd of pA, so |t1| <= |pB - b0| <= Ol + Ma + maxd + Bl: pB is within 2U (Ol + Ma + maxd + Bl)
+// + U Bl of the line, whatever the pair's angle.  So |pA - pB| >= D(C, B) - delta - eps with
+// eps = U (12 Ma + 3 Ol + 3 Bl + 2 maxd) <= U (21 omax + 3 Bl + 2 maxd) (omax bounds max|o_i| + Ma
+// over the lanes, Ol <= 3 max|o_i|), and the reference's rounded distance is >= maxd whenever
+// D(C, B) > maxd (1 + 5U) + delta + eps.  D(C, B) = |t.n| / |n| is evaluated with fmas (error
+// <= 8U |t|_1, absorbed by the 1e-6 |t|_1 slack; |n| rounded up), only for |n|^2 >= 1e-2.  Margin
+// mode 1 uses twice eps: 2.5e-6 omax + 3.6e-7 Bl + 2.4e-7 maxd + 1e-6; mode 0 keeps round 2's
+// 2e-5 (omax + bmax + 10 |t|_1 + maxd + 1) + 2e-6 and the 1e-4 relative factor.
+__device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float maxd, int margin) {
     if (!(K.delta < 1e30f)) return false;
     const f3 t = sub3(b0, K.co);
     const f3 n = mk(__builtin_fmaf(K.cu.y, bu.z, -(K.cu.z * bu.y)), __builtin_fmaf(K.cu.z, bu.x, -(K.cu.x * bu.z)),
@@ -273,11 +284,17 @@ __device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float 
     if (!(nn >= 1e-2f)) return false;
     const float tn = fabsf(__builtin_fmaf(t.x, n.x, __builtin_fmaf(t.y, n.y, t.z * n.z)));
     const float tl = fabsf(t.x) + fabsf(t.y) + fabsf(t.z);
-    const float bmax = fmaxf(fmaxf(fabsf(b0.x), fabsf(b0.y)), fabsf(b0.z));
-    const float mag = K.omax + bmax + 10.0f * tl + maxd + 1.0f;
-    const float eps = 1e-5f * mag + 1e-6f;
+    float lim;
+    if (margin) {
+        const float b1 = fabsf(b0.x) + fabsf(b0.y) + fabsf(b0.z);
+        lim = (maxd + K.delta) * 1.000001f + (2.5e-6f * K.omax + 3.6e-7f * b1 + 2.4e-7f * maxd + 1e-6f);
+    } else {
+        const float bmax = fmaxf(fmaxf(fabsf(b0.x), fabsf(b0.y)), fabsf(b0.z));
+        const float mag = K.omax + bmax + 10.0f * tl + maxd + 1.0f;
+        lim = (maxd + K.delta) * 1.0001f + 2.0f * (1e-5f * mag + 1e-6f);
+    }
     const float nl = __builtin_amdgcn_sqrtf(nn) * 1.000001f;
-    return (tn - 1e-6f * tl) > ((maxd + K.delta) * 1.0001f + 2.0f * eps) * (nl + 1e-6f);
+    return (tn - 1e-6f * tl) > lim * (nl + 1e-6f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -308,27 +325,45 @@ __device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float 
 //   t.n = au.(bu x b0) - bu.(o x au) = au.m0 - bu.q,
 // so per (lane, beam) only two dot products and c = au.bu remain: m0 is held per beam, q per lane.
 // |n|^2 = |au|^2|bu|^2 - c^2 (Lagrange) is bracketed by 0.99999 - c^2 <= |n|^2 <= 1.00001 - c^2
-// (unit vectors to ~1e-7, c to ~5e-7).  The computed t.n is within 1e-5 (bmax + omax) + 1e-6 of
-// the exact one (~2e-6 (bmax + omax) by the float error of the cross and dot products), and the
-// coordinate bound mag of far_from_lines uses tl <= |b0|_1 + |o|_1, so its margins split into a
-// beam part (Ab, Eb) and a lane part (Al, El):
-//   reject  <=>  tn > (Eb + El) + (Ab + Al) * nl,   nl = sqrt(nn_hi) * 1.000001 + 1e-6
-// which implies the line-line distance exceeds maxd * 1.0001 + 2 eps with eps >= far_from_lines'
-// eps: the same proof that every reference-computed distance of the pair is >= maxd.  A rejected
-// pair has nn_lo >= 1e-2, so nl > 0.1 and Eb + El < 10 (Eb + El) nl: the single-margin test
-//   reject  <=>  tn > (Ab' + Al') * nl,   Ab' = Ab + 10 Eb,  Al' = Al + 10 El
-// rejects a subset of those pairs (still a proof).  Near-parallel pairs (|n|^2 possibly < 1e-2) and
-// zero-length segments (Al' = FLT_MAX) are never rejected.
+// (unit vectors to ~1e-7, c to ~5e-7).  A pair is rejected only when |n|^2 >= 1e-2 (|n| > 0.0999)
+// and |t.n| > thr |n| with thr = Ab' + Al' (scan_need evaluates this without a square root).
+//
+// Margins (margin mode 1, the default since round 3).  U = 2^-24; L1 norms Ol = |o|_1, Bl = |b0|_1;
+// Ma = |A|, Mb = |B|.  D = |t.n| / |n| is the exact distance of the lines o + s au and b0 + s bu (the
+// stored float vectors, exact arithmetic).  Every point ComputeClosestPoints (photonbeam.cpp:87-186)
+// returns lies near one of those lines:
+//   * pA = a0 + au t0 with t0 in [0, Ma], or a0 + au d with d in [0, Ma]: the float products and sums
+//     move it at most 2U Ma + U Ol off the line; pA = a0 is on it; pA = a1 is within 10U Ma of it
+//     (au is (a1 - a0) rounded, scaled by the rounded 1 / |A|: a few U of direction);
+//   * pB = b0 + bu d with d in [0, Mb]: within 2U Mb + U Bl; pB = b0 + bu t1 (the quirk of :178-181,
+//     t1 outside [0, Mb]): within 2U |t1| + U Bl, and with |n| > 0.0999 the closest-point parameter
+//     is |t1| <= |t| / |n| <= 10.1 (Bl + Ol) (the float Cramer solution adds ~100U |t|), so
+//     within 20.2U (Bl + Ol) + U Bl.
+// So |pA - pB| >= D - eps, eps = U (21.2 (Bl + Ol) + 10 Ma + 2 Mb), and the reference's float
+// distance (difference, three squares, sum, correctly rounded sqrt) is >= (D - eps)(1 - 4U): it is
+// >= maxd whenever D >= maxd (1 + 5U) + eps.  The scan's t.n = x - bu.q (m0 = bu x b0 and q = o x au
+// rounded, two 3-term fma dot products) is within Et = 14U (Bl + Ol) of the exact t.n, so a reject
+// (|t.n|_computed > thr |n|) gives D > thr - Et / |n| >= thr - 140.1U (Bl + Ol).  Hence
+//   thr >= maxd (1 + 5U) + U (161.3 (Bl + Ol) + 10 Ma + 2 Mb)
+// proves that every reference-computed distance of a rejected pair is >= maxd.  The kernel uses
+// twice the U terms: Ab' = maxd * 1.000001 + 1.93e-5 Bl + 2.4e-7 Mb + 1e-6 (the absolute 1e-6 keeps
+// thr clear of underflow), Al' = 1.93e-5 Ol + 1.2e-6 Ma.  For a unit-box scene that is ~6e-5 over
+// maxd -- margin mode 0 (the round-2 bound, 2e-5 (omax + 10 |o|_1) + 1e-4 omax on each side) added
+// ~1.4e-3, which at the late C2 iterations (maxd ~ 3e-3) queued ~1.4x the contributing pairs.
+// Near-parallel pairs (|n|^2 possibly < 1e-2) and zero-length segments (Al' = FLT_MAX) are never
+// rejected.  tests/test_margin_bound.py checks the bound against the oracle's ComputeClosestPoints on
+// pairs placed just outside the threshold.
 struct ScanLane {
     f3 q;       // o x au
-    float al;   // Al' = 2e-5 (omax + 10 |o|_1) + 1e-4 omax;  FLT_MAX for a zero-length segment
+    float al;   // Al' (see above);  FLT_MAX for a zero-length segment
 };
 
-__device__ __forceinline__ ScanLane make_scan_lane(const Lane &L) {
+__device__ __forceinline__ ScanLane make_scan_lane(const Lane &L, int margin) {
     ScanLane S;
     S.q = mk(L.o.y * L.au.z - L.o.z * L.au.y, L.o.z * L.au.x - L.o.x * L.au.z, L.o.x * L.au.y - L.o.y * L.au.x);
     const float o1 = fabsf(L.o.x) + fabsf(L.o.y) + fabsf(L.o.z);
-    S.al = L.mag_a == 0.0f ? FLT_MAX : 2e-5f * (L.omax + 10.0f * o1) + 1e-4f * L.omax;
+    const float al = margin ? 1.93e-5f * o1 + 1.2e-6f * L.mag_a : 2e-5f * (L.omax + 10.0f * o1) + 1e-4f * L.omax;
+    S.al = L.mag_a == 0.0f ? FLT_MAX : al;
     return S;
 }
 
@@ -338,55 +373,64 @@ struct ScanBeam {
     float ab;
 };
 
-__device__ __forceinline__ ScanBeam make_scan_beam(const BeamV &r, float R) {
+__device__ __forceinline__ ScanBeam make_scan_beam(const BeamV &r, float R, int margin) {
     const float maxd = R + r.radius;
     ScanBeam B;
     B.bu = r.bu;
     B.m0 = mk(r.bu.y * r.b0.z - r.bu.z * r.b0.y, r.bu.z * r.b0.x - r.bu.x * r.b0.z, r.bu.x * r.b0.y - r.bu.y * r.b0.x);
-    const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
     const float b1 = fabsf(r.b0.x) + fabsf(r.b0.y) + fabsf(r.b0.z);
-    // Ab = maxd 1.0001 + 2e-5 (bmax + 10 |b0|_1) + 2e-6, Eb = 1e-5 bmax + 1e-6
-    B.ab = maxd * 1.0001f + 2e-5f * (bmax + 10.0f * b1) + 2e-6f + 10.0f * (1e-5f * bmax + 1e-6f);
+    if (margin) {
+        B.ab = maxd * 1.000001f + 1.93e-5f * b1 + 2.4e-7f * r.mag_b + 1e-6f;
+    } else {
+        const float bmax = fmaxf(fmaxf(fabsf(r.b0.x), fabsf(r.b0.y)), fabsf(r.b0.z));
+        // Ab = maxd 1.0001 + 2e-5 (bmax + 10 |b0|_1) + 2e-6, Eb = 1e-5 bmax + 1e-6
+        B.ab = maxd * 1.0001f + 2e-5f * (bmax + 10.0f * b1) + 2e-6f + 10.0f * (1e-5f * bmax + 1e-6f);
+    }
     return B;
 }
 
-// Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128).  The second
-// record's w is a stored 0 added to Ab': without a use the compiler narrows that read to
-// ds_read_b96, which takes 8 LDS cycles per wave instead of ds_read_b128's 4 (MI355X_MICROARCH.md
-// §LDS); Ab' + 0 == Ab' (Ab' > 0).
-__device__ __forceinline__ ScanBeam scan_beam_lds(const float4 (*tile)[2], int j) {
+// Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128): (bu, thr_sq) and
+// (m0, 1.0001).  The stored constant is the u' constant of scan_need, so every loaded component has
+// a use (a read whose w is unused is narrowed to ds_read_b96: 8 LDS cycles per wave, not 4).
+struct ScanStaged {
+    f3 bu, m0;
+    float thr_sq;  // fl(thr * |thr|), thr = Ab' + the packet's max Al'; -inf: rejected; +inf: never
+    float uc;      // 1.0001
+};
+__device__ __forceinline__ ScanStaged scan_beam_lds(const float4 (*tile)[2], int j) {
     const float4 a = tile[j][0], b = tile[j][1];
-    ScanBeam B;
+    ScanStaged B;
     B.bu = mk(a.x, a.y, a.z);
-    B.ab = a.w + b.w;
+    B.thr_sq = a.w;
     B.m0 = mk(b.x, b.y, b.z);
+    B.uc = b.w;
     return B;
 }
 
-// The per-(lane, beam) prefilter as ONE comparison, so that its ballot is the compare's own lane
-// mask (no mask materialisation, no exec juggling in the queue push).  The pair is rejected iff
-//   nn_lo >= 1e-2  and  tn > (Ab' + Al') * |n|          (the separable bound above)
+// The per-(lane, beam) prefilter.  The pair is rejected iff
+//   |n|^2 >= ~1e-2  and  tn > thr * |n|          (the separable bound above)
 // and `need` is the complement.  Squares, no square root of |n|:
-//   reject  <=>  fl(tn * tn) > fl(fl(thr * |thr|) * u'),   thr = Ab' + al_eff,
-//                u' = fl(1.0001 - c^2) if nn_lo >= 1e-2, else +inf.
+//   reject  <=>  u >= 0.0101  and  fl(tn * tn) > fl(thr_sq * u),   u = fl(1.0001 - c^2).
+// thr is per BEAM: Ab' plus the largest Al' of the packet's lanes (>= each lane's own Al', so the
+// bound above still proves every reject), and thr_sq = fl(thr * |thr|) is staged with the tile.
 // For thr > 0 this implies tn > thr * |n| for the exact cross product n of the stored unit vectors:
-// by the bracket above |n|^2 <= 1.00001 - c^2, and u' >= (1.0001 - c^2)(1 - 2^-24) >= |n|^2 + 8.9e-5;
-// the three roundings are at most 3 * 2^-24 relative, so tn^2 > thr^2 u' (1 - 1.8e-7) > thr^2 |n|^2.
-// A rejected pair has |n|^2 >= 0.99999 - c^2 >= 1e-2 (bracket), so |n| > 0.1 and the Eb + El fold
-// above still holds.  No underflow can fake a reject: thr >= Ab' > 1.2e-5 and u' > 8.9e-5 keep the
-// right side >= 1e-14; an overflowing tn^2 really exceeds a finite right side; NaN compares keep the
-// pair.  The sign of thr carries two switches: al_eff = FLT_MAX (prefilter off) overflows
-// thr * |thr| to +inf, never a reject; thr = -inf (al_eff = -inf for a lane off the tile, or Ab' =
-// -inf staged for a beam the packet rejects / past the tile's end) makes the right side -inf, always
-// a reject (tn^2 is finite: the lanes and beams involved have finite coordinates).
-__device__ __forceinline__ bool scan_need(const ScanLane &S, float al_eff, f3 au, const ScanBeam &B) {
+// by the bracket above |n|^2 <= 1.00001 - c^2, and u >= (1.0001 - c^2)(1 - 2^-24) >= |n|^2 + 8.9e-5;
+// the three roundings are at most 3 * 2^-24 relative, so tn^2 > thr^2 u (1 - 1.8e-7) > thr^2 |n|^2.
+// u >= 0.0101 means c^2 <= 0.99 (to rounding), so |n|^2 >= 0.99999 - c^2 > 0.00999 (bracket):
+// |n| > 0.0999, as the margin bound requires.  No underflow can fake a reject: thr >= Ab' > 1e-6 and
+// u >= 0.0101 keep the right side >= 1e-14; an overflowing tn^2 really exceeds a finite right side;
+// NaN compares keep the pair.  thr_sq = +inf (prefilter off) is never a reject; thr_sq = -inf (a
+// beam the packet rejects, or past the tile's end) is always one (tn^2 is finite: the lanes and
+// beams involved have finite coordinates).  A zero-length segment (au = 0, q = 0) has tn = 0 and is
+// never rejected by a finite positive thr_sq.  Lanes off the tile are masked by the caller.
+// Returned as the wave's lane mask of pairs to keep: each compare's ballot is the compare's own
+// result mask, combined on the scalar unit (no bool materialisation in VALU).  All lanes must call.
+__device__ __forceinline__ unsigned long long scan_keep_mask(const ScanLane &S, f3 au, const ScanStaged &B) {
     const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
-    const float nn_lo = __builtin_fmaf(-c, c, 0.99999f);
-    const float u = (nn_lo >= 1e-2f) ? __builtin_fmaf(-c, c, 1.0001f) : INFINITY;
+    const float u = __builtin_fmaf(-c, c, B.uc);
     const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
     const float t = __builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x)));
-    const float thr = B.ab + al_eff;
-    return !((t * t) > (thr * fabsf(thr)) * u);
+    return ~(__ballot(u >= 0.0101f) & __ballot((t * t) > B.thr_sq * u));
 }
 
 constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
@@ -500,7 +544,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan) {
+    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan, int margin) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
     // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
@@ -538,7 +582,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     K.delta = FLT_MAX;
     K.gbox = FLT_MAX;
     if (prefilter && __ballot(valid) != 0ull) K = make_bundle(L, valid);
-    const ScanLane SL = make_scan_lane(L);
+    const ScanLane SL = make_scan_lane(L, margin);
+    // the largest lane margin Al' of the packet, folded into every beam's threshold at staging (a
+    // zero-length segment, Al' = FLT_MAX, is never rejected anyway: see scan_need)
+    const float al_max = uniform_f(wave_max(valid && SL.al < FLT_MAX ? SL.al : 0.f));
     sh.acc[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     __builtin_amdgcn_wave_barrier();
     int cand = 0;
@@ -553,12 +600,16 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
 
     // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
     // stores (branch-free), a lane that queues nothing into its own discard slot
-    const auto push = [&](bool need, int32_t e_beam, int32_t e_lane) {
-        const unsigned long long m = __ballot(need);
+    // (m: the wave-uniform lane mask of the entries to queue)
+    const int discard = kQueueCap + lane;
+    const auto push = [&](unsigned long long m, int32_t e_beam, int32_t e_lane) {
         if (m == 0ull) return;
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
-        sh.q[need ? rank : kQueueCap + lane] = QEntry{e_beam, e_lane};
+        // slot = lane in m ? rank : discard, as one v_cndmask on the scalar mask (every lane stores)
+        int slot;
+        asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(slot) : "v"(discard), "v"(rank), "s"(m));
+        sh.q[slot] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
         if (COUNT) pf.queued += __popcll(m);
         if (BRE_SCAN_STATS) ss_q += __popcll(m);
@@ -607,38 +658,38 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         bool keep = false;
         if (lane < nb) {
             const BeamV r = load_beam(recs, first + lane);
-            T = make_scan_beam(r, R);
+            T = make_scan_beam(r, R, margin);
             // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
             // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
             keep = !prefilter ||
-                   !(bundle_far(K, r.b0, r.bu, R + r.radius) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
+                   !(bundle_far(K, r.b0, r.bu, R + r.radius, margin) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
         }
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
         __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
-        // every lane writes (the transposed scan reads record `lane`): Ab' = -inf for a beam the packet
-        // rejects or past the tile's end (bu = m0 = 0), which scan_need always rejects
-        sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, keep ? T.ab : -INFINITY);
-        sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 0.f);
+        // every lane writes (the transposed scan reads record `lane`): thr_sq = -inf for a beam the
+        // packet rejects or past the tile's end (bu = m0 = 0), which scan_need always rejects; +inf
+        // with the prefilter off (never a reject)
+        const float thr = T.ab + al_max;
+        const float thr_sq = !keep ? -INFINITY : (prefilter ? thr * fabsf(thr) : INFINITY);
+        sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, thr_sq);
+        sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 1.0001f);
         __builtin_amdgcn_wave_barrier();
-        // the lane's threshold term (see scan_need): Al', FLT_MAX with the prefilter off (never a
-        // reject), -inf for a lane off the tile (always a reject)
-        const float al_on = prefilter ? SL.al : FLT_MAX;
-        const float al_eff = lane_on ? al_on : -INFINITY;
         if (COUNT) {
             pf.useful += __popcll(km);
             // every beam of the tile: the reference box test (candidates) and the pairs the
             // prefilters drop; the queue gets exactly the production survivors, in order
             for (int j = 0; j < nb; ++j) {
                 const bool kept = (km >> j) & 1ull;
-                const bool need = kept && scan_need(SL, al_eff, L.au, scan_beam_lds(sh.tile, j));
+                const unsigned long long mk_ = scan_keep_mask(SL, L.au, scan_beam_lds(sh.tile, j)) & onm;
+                const bool need = kept && ((mk_ >> lane) & 1ull);
                 const Box6 box = load_beam(recs, first + j).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                 if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
                 cand += hit;
                 pf.rejects += hit & !need;
-                if (kept) push(need, (int32_t)(cur_first + j), lane);
+                if (kept) push(mk_, (int32_t)(cur_first + j), lane);
                 drain();
             }
             return;
@@ -673,8 +724,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i), readlane_f(SL.q.z, i));
                 Si.al = 0.f;
                 const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i), readlane_f(L.au.z, i));
-                const bool need = scan_need(Si, readlane_f(al_on, i), aui, scan_beam_lds(sh.tile, lane));
-                push(need, (int32_t)(cur_first + lane), i);
+                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tile, lane)), (int32_t)(cur_first + lane), i);
                 drain();
             }
             if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
@@ -689,9 +739,12 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const bool two = todo != 0ull;
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
-            const ScanBeam B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
-            const bool n1 = BRE_ABLATE == 3 ? lane_on && ((j1 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B1);
-            const bool n2 = BRE_ABLATE == 3 ? lane_on && ((j2 * 7 + lane) & 7) == 0 : scan_need(SL, al_eff, L.au, B2);
+            const ScanStaged B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
+            // lane masks: every lane evaluates both tests, the lanes off the tile are masked out
+            const unsigned long long n1 =
+                (BRE_ABLATE == 3 ? __ballot(((j1 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B1)) & onm;
+            const unsigned long long n2 =
+                (BRE_ABLATE == 3 ? __ballot(((j2 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B2)) & onm;
             push(n1, (int32_t)(cur_first + j1), lane);
             if (two) push(n2, (int32_t)(cur_first + j2), lane);
             drain();
@@ -1117,7 +1170,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan)
+                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

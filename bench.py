@@ -90,6 +90,7 @@ def parse(argv=None):
     ap.add_argument("--block-map", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--beam-key", type=int, default=-1, help=argparse.SUPPRESS)  # tree build key study (option 110)
+    ap.add_argument("--margin", type=int, default=-1, help=argparse.SUPPRESS)  # prefilter margin A/B (option 111)
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
@@ -215,6 +216,8 @@ def main():
             c.set_option(108, args.tscan)
         if args.beam_key >= 0:
             c.set_option(110, args.beam_key)
+        if args.margin >= 0:
+            c.set_option(111, args.margin)
         # one explicit stream per context, shared with torch: the HIP events that time the gather
         # kernel are recorded on the stream the kernel runs on
         st = torch.cuda.Stream(dev)
