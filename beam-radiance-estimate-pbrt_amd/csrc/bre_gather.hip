@@ -68,6 +68,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
 #endif
+// BRE_EXACT_SHFL 1: the exact stage takes the pair's segment o, tmax, 1/d, au and has_inf from the
+// segment's own lane by ds_bpermute instead of loading three SegRec planes (texture-path relief)
+#ifndef BRE_EXACT_SHFL
+#define BRE_EXACT_SHFL 0
+#endif
 // BRE_SCAN_STATS 1 (profiling builds only): the production tile kernel adds, per wave, scan-shape
 // sums into the counter block instead (profiles/scan_stats.py): lanes on the tile (candidates), kept
 // beams (contributions), scan steps taken (node_visits), steps of a full (lane, beam) pair
@@ -177,6 +182,8 @@ struct Bundle {
     // gbox = FLT_MAX disables the box reject
     float s0, s1, gbox;
     f3 icu;       // 1 / cu with infinities replaced by +-FLT_MAX
+    f3 q;         // co x cu (the separable line reject, bundle_far_sep)
+    float col1;   // |co|_1
 };
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -238,6 +245,8 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
     K.s0 = uniform_f(K.s0);
     K.s1 = uniform_f(K.s1);
     K.icu = mk(uniform_f(K.icu.x), uniform_f(K.icu.y), uniform_f(K.icu.z));
+    K.q = mk(K.co.y * K.cu.z - K.co.z * K.cu.y, K.co.z * K.cu.x - K.co.x * K.cu.z, K.co.x * K.cu.y - K.co.y * K.cu.x);
+    K.col1 = fabsf(K.co.x) + fabsf(K.co.y) + fabsf(K.co.z);
     return K;
 }
 
@@ -295,6 +304,24 @@ __device__ __forceinline__ bool bundle_far(const Bundle &K, f3 b0, f3 bu, float 
     }
     const float nl = __builtin_amdgcn_sqrtf(nn) * 1.000001f;
     return (tn - 1e-6f * tl) > lim * (nl + 1e-6f);
+}
+
+// The same packet-level line reject in the scan's separable form (margin mode 1): the bundle line
+// C = (co, cu) plays a lane whose margin is delta, so t.n = cu.m0 - bu.(co x cu) reuses the beam's
+// staged m0 = bu x b0 and |n|^2 is bracketed by c = cu.bu, no cross product or square root per beam.
+// The computed t.n is within 14U (Bl + |co|_1) of the exact one (the ScanLane analysis with o -> co,
+// au -> cu), i.e. D(C, B) within 140.1U (Bl + |co|_1) for |n| > 0.0999 (u >= 0.0101); with eps above,
+// rejecting D(C, B) > thr_b = (maxd + delta) 1.000001 + 1.93e-5 (Bl + |co|_1) + 2.5e-6 omax + 2.4e-7 Mb
+// + 1e-6 (twice both terms) proves every lane's reference distance >= maxd.  delta = FLT_MAX (the
+// reject disabled) squares to +inf: never a reject.
+__device__ __forceinline__ bool bundle_far_sep(const Bundle &K, f3 b0, f3 bu, f3 m0, float maxd, float mag_b) {
+    const float c = __builtin_fmaf(K.cu.x, bu.x, __builtin_fmaf(K.cu.y, bu.y, K.cu.z * bu.z));
+    const float u = __builtin_fmaf(-c, c, 1.0001f);
+    const float x = __builtin_fmaf(K.cu.x, m0.x, __builtin_fmaf(K.cu.y, m0.y, K.cu.z * m0.z));
+    const float t = __builtin_fmaf(-bu.x, K.q.x, __builtin_fmaf(-bu.y, K.q.y, __builtin_fmaf(-bu.z, K.q.z, x)));
+    const float b1 = fabsf(b0.x) + fabsf(b0.y) + fabsf(b0.z);
+    const float thr = (maxd + K.delta) * 1.000001f + 1.93e-5f * (b1 + K.col1) + 2.5e-6f * K.omax + 2.4e-7f * mag_b + 1e-6f;
+    return (u >= 0.0101f) & ((t * t) > (thr * thr) * u);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -456,7 +483,7 @@ struct TileShared {
 __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
                                            const float *__restrict__ sd, int64_t seg0,
                                            const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
-                                           bool count) {
+                                           bool count, const Lane &L) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
     const QEntry e = sh.q[first + (on ? lane : 0)];  // off lanes (a partial batch) read a valid entry
@@ -466,9 +493,28 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     // pass the box test, so the second half is rarely wasted)
     const float4 *sr = seg_plane(srec, seg0 + sl, 0);  // packet-plane layout: plane k at sr[64 k]
     const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
+#if BRE_EXACT_SHFL
+    // the segment's o, tmax, 1/d (sanitised), au and has_inf are resident in lane sl's registers:
+    // fetched by ds_bpermute (LDS crossbar) instead of three of the four SegRec loads (texture path)
+    (void)sd;
+    const int sa = sl << 2;
+    const auto shf = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(v))); };
+    const float4 s1 = sr[64], bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
+    const float4 pv = pw[b];
+    const float4 s0 = make_float4(shf(L.o.x), shf(L.o.y), shf(L.o.z), shf(L.tmax));
+    const float4 s3 = make_float4(shf(L.invs.x), shf(L.invs.y), shf(L.invs.z), 0.f);
+#if BRE_EXACT_SHFL == 2
+    const float4 s2 = sr[128];  // 2: only the box-test values by ds_bpermute
+#else
+    const float4 s2 = make_float4(shf(L.au.x), shf(L.au.y), shf(L.au.z),
+                                  __int_as_float(__builtin_amdgcn_ds_bpermute(sa, L.has_inf ? 1 : 0)));
+#endif
+#else
+    (void)L;
     const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
     const float4 s1 = sr[64], s2 = sr[128], bz = rb[2], bw = rb[3];
     const float4 pv = pw[b];
+#endif
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
     const float tmax = s0.w;
@@ -623,7 +669,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         int h = 0;
         while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, R, count_c);
+            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, R, count_c, L);
             h += 64;
             __builtin_amdgcn_wave_barrier();
         }
@@ -662,7 +708,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
             // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
             keep = !prefilter ||
-                   !(bundle_far(K, r.b0, r.bu, R + r.radius, margin) || (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
+                   !((margin ? bundle_far_sep(K, r.b0, T.bu, T.m0, R + r.radius, r.mag_b)
+                             : bundle_far(K, r.b0, r.bu, R + r.radius, 0)) ||
+                     (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
         }
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
@@ -861,7 +909,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, R, count_c);
+            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, R, count_c, L);
         }
         t1 = 0;
     }

@@ -111,9 +111,9 @@ def test_tight_margins_never_drop_a_reference_contribution(offset, size):
     assert worst > 0.25, worst
 
 
-def bundle_reject(o, p, au, mag_a, b0, bu, maxd):
-    """bundle_far (margin mode 1) for one packet: make_bundle's line C and delta in float32, then
-    the packet-level line reject of each beam."""
+def bundle_reject(o, p, au, mag_a, b0, bu, maxd, mag_b):
+    """bundle_far_sep (margin mode 1) for one packet: make_bundle's line C and delta in float32,
+    then the packet-level line reject of each beam in the separable form."""
     co = (o.astype(np.float64).mean(0)).astype(f32)
     su = au.astype(np.float64).sum(0)
     cu = (su / np.linalg.norm(su)).astype(f32)
@@ -125,19 +125,19 @@ def bundle_reject(o, p, au, mag_a, b0, bu, maxd):
     omax = float((np.abs(o).max(1) + mag_a).max())
     cm = float(np.abs(co).max())
     delta = f32(max(perp(o).max(), perp(p).max()) * 1.0001 + 1e-5 * (omax + cm) + 1e-6)
-    t = (b0 - co).astype(f32)
+    # bundle_far_sep: the separable form on the staged m0 = bu x b0 and q = co x cu
     cuv = np.broadcast_to(cu, bu.shape)
-    n = np.stack([fma32(cuv[:, 1], bu[:, 2], -(cuv[:, 2] * bu[:, 1]).astype(f32)),
-                  fma32(cuv[:, 2], bu[:, 0], -(cuv[:, 0] * bu[:, 2]).astype(f32)),
-                  fma32(cuv[:, 0], bu[:, 1], -(cuv[:, 1] * bu[:, 0]).astype(f32))], -1)
-    nn = fma32(n[:, 0], n[:, 0], fma32(n[:, 1], n[:, 1], (n[:, 2] * n[:, 2]).astype(f32)))
-    tn = np.abs(fma32(t[:, 0], n[:, 0], fma32(t[:, 1], n[:, 1], (t[:, 2] * n[:, 2]).astype(f32))))
-    tl = np.abs(t).sum(1).astype(f32)
+    m0 = cross_f32(bu, b0)
+    q = cross_f32(co[None, :], cu[None, :])[0]
+    c = fma32(cuv[:, 0], bu[:, 0], fma32(cuv[:, 1], bu[:, 1], (cuv[:, 2] * bu[:, 2]).astype(f32)))
+    u = fma32(-c, c, f32(1.0001))
+    x = fma32(cuv[:, 0], m0[:, 0], fma32(cuv[:, 1], m0[:, 1], (cuv[:, 2] * m0[:, 2]).astype(f32)))
+    t = fma32(-bu[:, 0], q[0], fma32(-bu[:, 1], q[1], fma32(-bu[:, 2], q[2], x)))
     b1 = np.abs(b0).sum(1).astype(f32)
-    lim = ((maxd + delta) * f32(1.000001) + (f32(2.5e-6) * f32(omax) + f32(3.6e-7) * b1 + f32(2.4e-7) * maxd
-                                             + f32(1e-6))).astype(f32)
-    nl = (np.sqrt(nn) * f32(1.000001)).astype(f32)
-    return (nn >= f32(1e-2)) & ((tn - f32(1e-6) * tl) > lim * (nl + f32(1e-6))), delta, co, cu
+    col1 = f32(np.abs(co).sum())
+    thr = ((maxd + delta) * f32(1.000001) + f32(1.93e-5) * (b1 + col1) + f32(2.5e-6) * f32(omax)
+           + f32(2.4e-7) * mag_b + f32(1e-6)).astype(f32)
+    return (u >= f32(0.0101)) & ((t * t).astype(f32) > ((thr * thr).astype(f32) * u).astype(f32)), delta, co, cu
 
 
 @pytest.mark.parametrize("offset,size,spread", [(0.0, 1.0, 0.02), (5.0, 1.0, 0.2), (-80.0, 4.0, 0.05)])
@@ -162,13 +162,13 @@ def test_tight_bundle_margins_never_drop_a_reference_contribution(offset, size, 
         v[: nb // 4] = dirn + 1e-3 * rng.normal(size=(nb // 4, 3))  # near-parallel to the packet
         v /= np.linalg.norm(v, axis=1, keepdims=True)
         # a first pass fixes C and delta; beams are then placed at D(C, B) around delta + maxd
-        _, delta, co, cu = bundle_reject(o, p, au, mag_a, o[:1], au[:1], maxd)
+        _, delta, co, cu = bundle_reject(o, p, au, mag_a, o[:1], au[:1], maxd, mag_a[:1])
         cud = cu.astype(np.float64)
         nvec = np.cross(cud, v)
         ok = np.linalg.norm(nvec, axis=1) > 0.105
         nh = nvec / np.maximum(np.linalg.norm(nvec, axis=1, keepdims=True), 1e-30)
         c1 = float(np.abs(c0).sum()) + 2 * size
-        m_est = 2.5e-6 * (np.abs(c0).max() + 2 * size) + 3.6e-7 * c1 + 1e-6 * c1 + 1e-6
+        m_est = 2.5e-6 * (np.abs(c0).max() + 2 * size) + 1.93e-5 * 2 * c1 + 1e-6
         D = (float(delta) + float(maxd)) * 1.000001 + m_est * rng.uniform(-1.0, 4.0, nb)
         s0 = rng.uniform(-0.2, 1.2, nb) * L
         pc = co.astype(np.float64) + cud * s0[:, None] + nh * D[:, None]
@@ -176,8 +176,8 @@ def test_tight_bundle_margins_never_drop_a_reference_contribution(offset, size, 
         t1 = Lb * rng.uniform(-0.6, 1.6, nb)
         b0 = (pc - v * t1[:, None]).astype(f32)
         b1 = (pc + v * (Lb - t1)[:, None]).astype(f32)
-        bu, _ = unit_f32(b0, b1)
-        rej, _, _, _ = bundle_reject(o, p, au, mag_a, b0, bu, np.full(nb, maxd, f32))
+        bu, mag_b = unit_f32(b0, b1)
+        rej, _, _, _ = bundle_reject(o, p, au, mag_a, b0, bu, np.full(nb, maxd, f32), mag_b)
         rej &= ok
         rejected += int(rej.sum())
         for j in np.nonzero(rej)[0]:
