@@ -64,6 +64,7 @@ struct bre_ctx {
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
+    int tile_axis = 0;       // internal: tile kernel tile axis reject (GatherArgs::tileax), 1 = on (measured slower)
     int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
@@ -92,7 +93,7 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
-    DevMem counters_buf, roots, partial, pcnt, segrec;
+    DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
@@ -465,6 +466,13 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)chunk * (size_t)c->split));
         a.pcnt = c->pcnt.as<int32_t>();
     }
+    if (c->tile_axis && a.leaf_size > 0) {
+        const int64_t ntiles = (c->nvalid + a.leaf_size - 1) / a.leaf_size;
+        HIPCHK(c, c->tileax.ensure(sizeof(TileAxis) * (size_t)ntiles));
+        HIPCHK(c, c->segbox.ensure(sizeof(unsigned int) * 8));
+        a.tileax = c->tileax.as<TileAxis>();
+        a.segbox = c->segbox.as<unsigned int>();
+    }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
     for (int64_t off = 0; off < nseg; off += chunk) {
         GatherArgs ac = a;
@@ -556,6 +564,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
+                     &c->tileax, &c->segbox,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -659,6 +668,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)
         if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
         c->tscan = (int)value;
+        return BRE_OK;
+    case 112:  // internal: tile kernel tile axis reject, 1 on / 0 off (default; A/B)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0 or 1");
+        c->tile_axis = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");

@@ -125,6 +125,14 @@ __device__ __forceinline__ const float4 *seg_plane(const SegRec *base, int64_t s
     return reinterpret_cast<const float4 *>(base) + ((s >> 6) << 8) + (k << 6) + (s & 63);
 }
 
+// Per leaf tile of the tile kernel's tree, per gather (k_tile_axis): an axis line p + s d (|d| = 1)
+// such that every beam LINE of the tile, clipped to the box of the gather's segments grown by
+// (R + rmax) and a margin, lies within rho of it.  rho < 0: the tile cannot contribute at all.
+struct alignas(16) TileAxis {
+    float p[3], rho;
+    float d[3], rmax;  // rmax: the tile's largest beam radius
+};
+
 struct GatherArgs {
     int64_t nseg;
     const float *o, *p, *d, *tmax;
@@ -153,6 +161,8 @@ struct GatherArgs {
     int block_map;         // tile kernel block -> (packet, subtree) mapping (k_gather_tile)
     int tscan;             // tile kernel: transposed scan when on-lanes * 8 < kept beams * tscan (0: off)
     int margin;            // tile kernel prefilter margins: 1 = the tight bound (default), 0 = round 2's
+    TileAxis *tileax;      // tile kernel: per-tile axis bounds (ntiles), null = no tile axis reject
+    unsigned int *segbox;  // tile kernel: 6 ordered uints of scratch (the launch's segment box)
 };
 
 // capsule-chunk index (bre_chunk.hip)

@@ -37,7 +37,8 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // Profiling ablations (compile-time, off in the product; profiles/variant.sh builds them into
 // separate libraries): BRE_ABLATE 2 = no exact stage (queue drained unread), 3 = no prefilter scan
 // (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
-// tiles not scanned).
+// tiles not scanned), 5 = exact stage accumulates in one racy RMW round instead of the ordered rank
+// rounds (wrong sums: the price of the ordering).
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
 #endif
@@ -73,6 +74,20 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_EXACT_SHFL
 #define BRE_EXACT_SHFL 0
 #endif
+// BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes and the power through buffer
+// descriptors (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer
+// math; C2 +0.8%, C3 +2%, profiles/r3b/run4)
+#ifndef BRE_BUF_LOADS
+#define BRE_BUF_LOADS 1
+#endif
+// Raw buffer resource over [p, p + 4 GiB): offsets are 32-bit, out-of-range reads return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_f4(__amdgpu_buffer_rsrc_t r, unsigned int voff, unsigned int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+}
 // BRE_SCAN_STATS 1 (profiling builds only): the production tile kernel adds, per wave, scan-shape
 // sums into the counter block instead (profiles/scan_stats.py): lanes on the tile (candidates), kept
 // beams (contributions), scan steps taken (node_visits), steps of a full (lane, beam) pair
@@ -325,6 +340,176 @@ __device__ __forceinline__ bool bundle_far_sep(const Bundle &K, f3 b0, f3 bu, f3
 }
 
 // ---------------------------------------------------------------------------------------------
+// Tile axis reject (option 112, OFF by default: measured -2..-3% at C2, +-1% at C3, profiles/r3b/run5-6;
+// the tiles it skips are almost all tiles whose beams the packet rejects anyway, so it saves only
+// their staging, and the per-gather axis pass + per-leaf test cost more).  A contributing pair (lane i, beam j) has the reference's pA on segment i (to
+// rounding) and its pB on beam j's line with |pA - pB| < maxd_j, so pB lies in the box of the
+// launch's segments grown by maxd_j.  If every beam line of a tile, clipped to that box (plus a
+// margin), lies within rho of the tile's axis line (k_tile_axis: distance to a line is convex along
+// a line, so the clipped piece's two end points bound it), then dist(pB, axis) <= rho, while
+// dist(pA, C) <= delta (the packet's bundle line); hence D(C, axis) <= rho + delta + maxd_j for
+// any contributing pair, and a tile with D(C, axis) > rho + delta + maxd_max (+ margins) holds no
+// pair that can contribute to this packet: it is skipped without staging (the production
+// instantiation only: the counting one box-tests every beam of every visited tile for C).
+__device__ __forceinline__ unsigned int ord_u(float f) {
+    const unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord_f(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ void k_segbox_init(unsigned int *__restrict__ b) {
+    if (threadIdx.x < 6) b[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+}
+
+// box of the launch's finite segment end points (6 ordered uints: min xyz, max xyz)
+__global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__restrict__ o, const float *__restrict__ p,
+                                                unsigned int *__restrict__ b) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
+    if (i < nseg) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float *q = (e ? p : o) + 3 * i;
+            const float v[3] = {q[0], q[1], q[2]};
+            if (isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2])) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    mn[k] = min(mn[k], ord_u(v[k]));
+                    mx[k] = max(mx[k], ord_u(v[k]));
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], off));
+            mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(&b[k], mn[k]);
+            atomicMax(&b[3 + k], mx[k]);
+        }
+    }
+}
+
+// One wave per leaf tile: axis = mean start -> mean end of its usable beams, rho = the largest
+// distance of a clipped beam line's end points from the axis (with rounding margins).
+__global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ recs, int64_t nvalid, int leaf_size,
+                                                  const unsigned int *__restrict__ segb, float R,
+                                                  TileAxis *__restrict__ out) {
+    const int64_t tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t j = tile * leaf_size + lane;
+    bool ok = lane < leaf_size && j < nvalid;
+    f3 b0 = mk(0.f, 0.f, 0.f), bu = mk(0.f, 0.f, 0.f);
+    float mb = 0.f, rad = 0.f;
+    if (ok) {
+        const BeamV r = load_beam(recs, j);
+        b0 = r.b0;
+        bu = r.bu;
+        mb = r.mag_b;
+        rad = r.radius;
+        // a zero-length or non-finite beam has a NaN / infinite reference box: never a candidate
+        ok = mb > 0.f && isfinite(mb) && isfinite(b0.x) && isfinite(b0.y) && isfinite(b0.z) && isfinite(bu.x) &&
+             isfinite(bu.y) && isfinite(bu.z) && isfinite(rad);
+    }
+    const float rmax = wave_max(ok ? rad : 0.f);
+    const float n = wave_sum(ok ? 1.f : 0.f);
+    TileAxis A;
+    if (n == 0.f || !(segb[0] <= segb[3] && segb[1] <= segb[4] && segb[2] <= segb[5])) {
+        // no usable beam (or no finite segment): nothing of this tile can contribute
+        A.p[0] = A.p[1] = A.p[2] = 0.f;
+        A.d[0] = 1.f;
+        A.d[1] = A.d[2] = 0.f;
+        A.rho = -1.f;
+        A.rmax = rmax;
+        if (lane == 0) out[tile] = A;
+        return;
+    }
+    const f3 e = add3(b0, scale3(bu, mb));
+    const f3 ps = mk(wave_sum(ok ? b0.x : 0.f) / n, wave_sum(ok ? b0.y : 0.f) / n, wave_sum(ok ? b0.z : 0.f) / n);
+    const f3 pe = mk(wave_sum(ok ? e.x : 0.f) / n, wave_sum(ok ? e.y : 0.f) / n, wave_sum(ok ? e.z : 0.f) / n);
+    f3 d = sub3(pe, ps);
+    const float dl = sqrtf(lensq3(d));
+    d = (dl > 1e-6f * (1.f + fabsf(ps.x) + fabsf(ps.y) + fabsf(ps.z)) && isfinite(dl)) ? scale3(d, 1.f / dl)
+                                                                                      : mk(1.f, 0.f, 0.f);
+    // the region: segment box grown by maxd_max = R + rmax, plus margins
+    const float lo[3] = {ord_f(segb[0]), ord_f(segb[1]), ord_f(segb[2])};
+    const float hi[3] = {ord_f(segb[3]), ord_f(segb[4]), ord_f(segb[5])};
+    const float cm = fmaxf(fmaxf(fmaxf(fabsf(lo[0]), fabsf(lo[1])), fmaxf(fabsf(lo[2]), fabsf(hi[0]))),
+                           fmaxf(fabsf(hi[1]), fabsf(hi[2])));
+    const float grow = (R + rmax) * 1.001f + 1e-5f * cm + 1e-6f;
+    float dist = 0.f;
+    if (ok) {
+        const float o3[3] = {b0.x, b0.y, b0.z}, u3[3] = {bu.x, bu.y, bu.z};
+        float t0 = -FLT_MAX, t1 = FLT_MAX;
+        bool in = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float l = lo[k] - grow, h = hi[k] + grow;
+            if (u3[k] == 0.f) {
+                in = in && o3[k] >= l && o3[k] <= h;
+            } else {
+                float a = (l - o3[k]) / u3[k], c = (h - o3[k]) / u3[k];
+                if (a > c) {
+                    const float x = a;
+                    a = c;
+                    c = x;
+                }
+                t0 = fmaxf(t0, a);
+                t1 = fminf(t1, c);
+            }
+        }
+        if (in && t0 <= t1) {
+            // widen the piece by a little (the slab parameters carry rounding)
+            const float tw = 1e-5f * (fabsf(t0) + fabsf(t1)) + 1e-6f;
+            t0 -= tw;
+            t1 += tw;
+            const auto dax = [&](float t) {
+                const f3 q = sub3(add3(b0, scale3(bu, t)), ps);
+                const f3 c = mk(q.y * d.z - q.z * d.y, q.z * d.x - q.x * d.z, q.x * d.y - q.y * d.x);
+                return sqrtf(lensq3(c));
+            };
+            dist = fmaxf(dax(t0), dax(t1));
+            // a NaN distance must not shrink rho: treat it as unbounded
+            if (!(dist == dist)) dist = FLT_MAX;
+        }
+    }
+    const float rho = wave_max(dist);
+    const float pm = fmaxf(fmaxf(fabsf(ps.x), fabsf(ps.y)), fabsf(ps.z));
+    A.p[0] = ps.x;
+    A.p[1] = ps.y;
+    A.p[2] = ps.z;
+    A.d[0] = d.x;
+    A.d[1] = d.y;
+    A.d[2] = d.z;
+    A.rho = rho * 1.0001f + 1e-5f * (cm + pm + grow) + 1e-6f;
+    A.rmax = rmax;
+    if (lane == 0) out[tile] = A;
+}
+
+// D(C, axis) > rho + delta + maxd_max + margins (all wave-uniform).  Near-parallel axes (|n|^2 <
+// 1e-4, where the float cross product is too inexact to divide by) are never skipped.
+__device__ __forceinline__ bool tile_axis_far(const Bundle &K, const TileAxis *__restrict__ tax, int64_t tile, float R) {
+    const float4 *q = reinterpret_cast<const float4 *>(tax + tile);
+    const float4 a = q[0], b = q[1];
+    const f3 n = mk(K.cu.y * b.z - K.cu.z * b.y, K.cu.z * b.x - K.cu.x * b.z, K.cu.x * b.y - K.cu.y * b.x);
+    const float nn = lensq3(n);
+    const f3 w = mk(a.x - K.co.x, a.y - K.co.y, a.z - K.co.z);
+    const float wn = fabsf(dot3(w, n));
+    const float w1 = fabsf(w.x) + fabsf(w.y) + fabsf(w.z);
+    const float lim = a.w + K.delta + (R + b.w) * 1.001f + 1e-4f * w1 + 1e-5f;
+    return (a.w < 0.f) | ((nn >= 1e-4f) & (K.delta < 1e30f) & (wn > lim * sqrtf(nn) * 1.0001f));
+}
+
+// ---------------------------------------------------------------------------------------------
 // Kernel 0/4 (k_gather_tile): wave-packet traversal over leaf TILES of up to 64 beams.
 //
 // At dense candidate sets (the C2 Cornell fog: a camera segment passes ~16% of all beam boxes,
@@ -509,6 +694,15 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const float4 s2 = make_float4(shf(L.au.x), shf(L.au.y), shf(L.au.z),
                                   __int_as_float(__builtin_amdgcn_ds_bpermute(sa, L.has_inf ? 1 : 0)));
 #endif
+#elif BRE_BUF_LOADS
+    (void)L;
+    (void)sr;
+    // SegRec plane k of this packet at byte (seg0 / 64) * 4096 + k * 1024 + sl * 16 (packet-plane layout)
+    const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec), prs = buf_rsrc(pw);
+    const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
+    const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
+    const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
+    const float4 pv = buf_f4(prs, (unsigned int)b << 4, 0u);
 #else
     (void)L;
     const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
@@ -559,6 +753,17 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     // rounds, again in lane order.  (`count` only decides whether the count is used: it is always kept.)
     (void)count;
     if (__ballot(contrib) == 0ull) return;
+    if (BRE_ABLATE == 5) {  // timing ablation only: one racy read-modify-write round (sums are wrong)
+        if (contrib) {
+            float4 a = sh.acc[sl];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+            sh.acc[sl] = a;
+        }
+        return;
+    }
     sh.rk[lane] = 0;
     const int rank = contrib ? atomicAdd(&sh.rk[sl], 1) : BRE_RMW_MAX_RUNS + 64;
     for (int k = 0; k < BRE_RMW_MAX_RUNS; ++k) {
@@ -590,7 +795,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan, int margin) {
+    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan, int margin,
+    const TileAxis *__restrict__ tax) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
     // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
@@ -641,7 +847,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t cur_first = 0;     // first beam of the current leaf
     unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
     unsigned long long ss_on = 0, ss_kept = 0, ss_steps = 0, ss_pairs = 0, ss_leaves = 0, ss_q = 0, ss_min = 0,
-                       ss_tr = 0;
+                       ss_tr = 0, ss_skip = 0;
     const unsigned long long ph_t0 = phase_clock();
 
     // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
@@ -696,6 +902,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pf.beams += nb;
         }
         if (BRE_ABLATE == 4) return;
+        if (!COUNT && tax != nullptr) {
+            // skip the tile when no pair of it can contribute to this packet (tile_axis_far)
+            if (__builtin_amdgcn_readfirstlane((int)tile_axis_far(K, tax, (int64_t)(~c), R))) {
+                if (BRE_SCAN_STATS) ++ss_skip;
+                return;
+            }
+        }
         const unsigned long long l0 = phase_clock();
         cur_first = first;
         ScanBeam T;
@@ -1214,11 +1427,21 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     if (!a.segrec || a.leaf_size > 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
+    const TileAxis *tax = nullptr;
+    if (a.tileax && a.segbox && a.prefilter && a.nvalid > 0) {
+        const int64_t ntiles = (a.nvalid + a.leaf_size - 1) / a.leaf_size;
+        hipLaunchKernelGGL(k_segbox_init, dim3(1), dim3(64), 0, s, a.segbox);
+        hipLaunchKernelGGL(k_segbox, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
+                           a.segbox);
+        hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.nvalid, a.leaf_size,
+                           a.segbox, a.R, a.tileax);
+        tax = a.tileax;
+    }
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin)
+                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin, tax)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

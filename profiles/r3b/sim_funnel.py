@@ -20,6 +20,40 @@ pad = T * 64 - nb
 tlo = np.concatenate([blo, np.full((pad, 3), np.inf)]).reshape(T, 64, 3).min(1)
 thi = np.concatenate([bhi, np.full((pad, 3), -np.inf)]).reshape(T, 64, 3).max(1)
 bvec = be - bs; bmag = np.linalg.norm(bvec, axis=1); bu = bvec / np.where(bmag > 0, bmag, 1)[:, None]
+# tile axis lines (mean start -> mean end) and radius rho: every beam LINE, clipped to the region
+# R = segment bounds + maxd, lies within rho of the axis line (convexity: check the clip end points)
+Rlo = np.minimum(D["so"].min(0), D["sp"].min(0)) - 2 * R - 1e-4
+Rhi = np.maximum(D["so"].max(0), D["sp"].max(0)) + 2 * R + 1e-4
+padn = T * 64 - nb
+S_ = np.concatenate([bs, np.repeat(bs[-1:], padn, 0)]).reshape(T, 64, 3)
+E_ = np.concatenate([be, np.repeat(be[-1:], padn, 0)]).reshape(T, 64, 3)
+U_ = np.concatenate([bu, np.repeat(bu[-1:], padn, 0)]).reshape(T, 64, 3)
+ax0 = S_.mean(1); ax1 = E_.mean(1); axd = ax1 - ax0; axd /= np.linalg.norm(axd, axis=1, keepdims=True)
+invu = 1.0 / np.where(U_ == 0, 1e-30, U_)
+la = (Rlo - S_) * invu; lb = (Rhi - S_) * invu
+tin = np.minimum(la, lb).max(2); tout = np.maximum(la, lb).min(2)
+def dist_axis(P):
+    w = P - ax0[:, None, :]
+    return np.linalg.norm(np.cross(w, axd[:, None, :]), axis=2)
+Pin = S_ + U_ * tin[..., None]; Pout = S_ + U_ * tout[..., None]
+valid = tout > tin
+rho = np.where(valid, np.maximum(dist_axis(Pin), dist_axis(Pout)), 0).max(1)
+print("tile rho median %.3f p90 %.3f" % tuple(np.percentile(rho, [50, 90])))
+def group_axis(G):
+    # axis / rho over G consecutive tiles (a subtree of G leaves)
+    TG = T // G
+    Sg = S_[:TG * G].reshape(TG, G * 64, 3); Eg = E_[:TG * G].reshape(TG, G * 64, 3); Ug = U_[:TG * G].reshape(TG, G * 64, 3)
+    a0 = Sg.mean(1); a1 = Eg.mean(1); ad = a1 - a0; ad /= np.linalg.norm(ad, axis=1, keepdims=True)
+    iu = 1.0 / np.where(Ug == 0, 1e-30, Ug)
+    l1 = (Rlo - Sg) * iu; l2 = (Rhi - Sg) * iu
+    ti = np.minimum(l1, l2).max(2); to = np.maximum(l1, l2).min(2)
+    def da(P):
+        return np.linalg.norm(np.cross(P - a0[:, None, :], ad[:, None, :]), axis=2)
+    rg = np.where(to > ti, np.maximum(da(Sg + Ug * ti[..., None]), da(Sg + Ug * to[..., None])), 0).max(1)
+    return a0, ad, rg
+GA = {G: group_axis(G) for G in (2, 4)}
+for G in (2, 4):
+    print("group %d rho median %.3f" % (G, np.median(GA[G][2])))
 # segment order: Hilbert 6-D of (o, p)
 pts = np.concatenate([so, sp]); lo, hi = pts.min(0), pts.max(0)
 ks = hilbert_keys(np.concatenate([quant(so, lo, hi), quant(sp, lo, hi)], 1))
@@ -86,6 +120,24 @@ for pi in pk:
         miss_ = np.maximum(np.minimum(aa_, bb_).max(1), 0) > np.minimum(np.maximum(aa_, bb_).min(1), 1)
         return ~(far_ | miss_)
     tix = np.searchsorted(vis, idx // 64)
+    # tile-level axis reject: D(C, axis) > rho + delta + maxd
+    nax = np.cross(cu, axd[vis]); nnax = np.linalg.norm(nax, axis=1)
+    Dax = np.where(nnax > 1e-6, np.abs(((ax0[vis] - co) * nax).sum(1)) / np.maximum(nnax, 1e-12),
+                   np.linalg.norm(np.cross(ax0[vis] - co, cu), axis=1))
+    skip = Dax > rho[vis] + delta + 2 * R + 1e-4
+    kt = np.bincount(tix, weights=keep, minlength=len(vis))
+    add("tiles_axis_skip", int(skip.sum())); add("tiles_axis_skip_with_kept", int((skip & (kt > 0)).sum()))
+    add("kept_in_skipped", float(kt[skip].sum()))
+    for G in (2, 4):
+        a0, ad, rg = GA[G]
+        gi = vis // G
+        gi_ok = gi < len(rg)
+        gi = np.minimum(gi, len(rg) - 1)
+        nax2 = np.cross(cu, ad[gi]); nn2 = np.linalg.norm(nax2, axis=1)
+        D2 = np.where(nn2 > 1e-6, np.abs(((a0[gi] - co) * nax2).sum(1)) / np.maximum(nn2, 1e-12),
+                      np.linalg.norm(np.cross(a0[gi] - co, cu), axis=1))
+        sk2 = gi_ok & (D2 > rg[gi] + delta + 2 * R + 1e-4)
+        add(f"tiles_skip_by_group{G}", int(sk2.sum())); add(f"tiles_skip_by_tile_or_group{G}", int((sk2 | skip).sum()))
     for G in (2, 4):
         kg = np.stack([bundle_keep(slice(g * 64 // G, (g + 1) * 64 // G)) for g in range(G)])  # (G, nidx)
         # lane-steps: per tile max over groups of kept beams (one beam per group per step)
@@ -128,6 +180,8 @@ for k, v in tot.items():
     print(k, v)
 Q = tot[f"queued@{scales[0]}"]
 print("tiles with 0 kept %.3f, <=4 kept %.3f, on lanes per visited tile %.1f" % (tot["tiles_zero_kept"] / tot["tiles_visited"], tot["tiles_le4_kept"] / tot["tiles_visited"], tot["onlanes_per_tile"] / tot["tiles_visited"]))
+print("tile axis reject: %.3f of visited tiles skipped (%.3f of them had kept beams; kept beams dropped %.3f)" % (tot["tiles_axis_skip"] / tot["tiles_visited"], tot["tiles_axis_skip_with_kept"] / max(tot["tiles_axis_skip"], 1), tot["kept_in_skipped"] / tot["beams_kept"]))
+print("visited tiles skipped via their group of 2: %.3f, of 4: %.3f (union with tile test: %.3f / %.3f)" % tuple(tot[k] / tot["tiles_visited"] for k in ("tiles_skip_by_group2", "tiles_skip_by_group4", "tiles_skip_by_tile_or_group2", "tiles_skip_by_tile_or_group4")))
 print("beam-steps (x64 lanes) per packet: whole %.0f  2 groups %.0f  4 groups %.0f" % (tot["whole_beamsteps"] / npk, tot["g2_steps"] / npk, tot["g4_steps"] / npk))
 print("per packet: tiles %.0f staged %.0f kept %.0f (%.3f) lane_tests %.0f scan_steps %.0f" % (
     tot["tiles_visited"] / npk, tot["beams_staged"] / npk, tot["beams_kept"] / npk, tot["beams_kept"] / tot["beams_staged"],
