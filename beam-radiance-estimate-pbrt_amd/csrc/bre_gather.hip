@@ -74,6 +74,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_EXACT_SHFL
 #define BRE_EXACT_SHFL 0
 #endif
+// BRE_SQRT_NOSCALE 1 (default): the exact stage's two square roots without the compiler's small-input
+// scaling (sqrt_cr_noscale, bit-identical results: see tile_exact); 0 = sqrtf
+#ifndef BRE_SQRT_NOSCALE
+#define BRE_SQRT_NOSCALE 1
+#endif
 // BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes and the power through buffer
 // descriptors (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer
 // math; C2 +0.8%, C3 +2%, profiles/r3b/run4)
@@ -731,12 +736,25 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     bool contrib = false;
     if (hit) {
         const float maxd = R + bw.y;  // MaxDistance = currentBeamRadius + beam->radius
-        float dist;
-        const bool ok = closest_distance(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w, mk(by.z, by.w, bz.x),
-                                         mk(bz.y, bz.z, bz.w), bw.x, dist);
+        float d2, unused;
+        const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w,
+                                                        mk(by.z, by.w, bz.x), mk(bz.y, bz.z, bz.w), bw.x, d2, unused);
+        // |pA - pB| correctly rounded (photonbeam.cpp:500).  Without the compiler's small-input scaling
+        // when maxd >= 2^-30: for d2 >= 2^-96 the root is bit-identical; below, both roots are < 2^-47.9,
+        // so both pass dist < maxd and give r < 2^-17.9, r^2 < 2^-35 and 1 - r^2 == 1: the same value.
+#if BRE_SQRT_NOSCALE
+        const float dist = (maxd >= 0x1p-30f) ? sqrt_cr_noscale(d2) : sqrtf(d2);
+#else
+        const float dist = sqrtf(d2);
+#endif
         if (ok & (dist < maxd)) {
             const float rr = dist / maxd;
+            // 1 - fl(r^2) is 0 or >= 2^-24 (fl(r^2) <= 1 - 2^-24 unless it is 1): never in the scaled range
+#if BRE_SQRT_NOSCALE
+            const float w = sqrt_cr_noscale(1.0f - rr * rr);
+#else
             const float w = sqrtf(1.0f - rr * rr);
+#endif
             v.x = pv.x * w;
             v.y = pv.y * w;
             v.z = pv.z * w;
@@ -847,7 +865,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t cur_first = 0;     // first beam of the current leaf
     unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
     unsigned long long ss_on = 0, ss_kept = 0, ss_steps = 0, ss_pairs = 0, ss_leaves = 0, ss_q = 0, ss_min = 0,
-                       ss_tr = 0, ss_skip = 0;
+                       ss_tr = 0;
     const unsigned long long ph_t0 = phase_clock();
 
     // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
@@ -905,7 +923,6 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         if (!COUNT && tax != nullptr) {
             // skip the tile when no pair of it can contribute to this packet (tile_axis_far)
             if (__builtin_amdgcn_readfirstlane((int)tile_axis_far(K, tax, (int64_t)(~c), R))) {
-                if (BRE_SCAN_STATS) ++ss_skip;
                 return;
             }
         }

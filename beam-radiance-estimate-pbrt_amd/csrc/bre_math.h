@@ -142,7 +142,9 @@ __host__ __device__ __forceinline__ bool node_test(const Box6 &b, f3 o, f3 invs,
 // With WANT_S, also returns the beam-line parameter s of the returned beam point, pB = b0 + bu*s
 // (t1 when t0 is inside A, else the clamped projection of A's endpoint): the capsule-chunk
 // index (bre_chunk.hip) assigns each pair to the chunk whose ownership interval holds s.
-template <bool WANT_S>
+// SQ: return the squared distance lensq3(aClosest - bClosest) instead of its square root (the caller
+// takes the correctly rounded root itself, e.g. sqrt_cr_noscale).
+template <bool WANT_S, bool SQ = false>
 __host__ __device__ __forceinline__ bool closest_distance_t(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu,
                                                             float mag_b, float &dist, float &s_out) {
     if (mag_a == 0.0f) {
@@ -150,7 +152,7 @@ __host__ __device__ __forceinline__ bool closest_distance_t(f3 a0, f3 a1, f3 au,
         const float d = dot3(sub3(a0, b0), bu);
         const float dc = clampf_ref(d, 0.0f, mag_b);
         const f3 bc = add3(b0, scale3(bu, dc));
-        dist = len3(sub3(a0, bc));
+        dist = SQ ? lensq3(sub3(a0, bc)) : len3(sub3(a0, bc));
         if (WANT_S) s_out = dc;
         return true;
     }
@@ -176,9 +178,25 @@ __host__ __device__ __forceinline__ bool closest_distance_t(f3 a0, f3 a1, f3 au,
         const float d = clampf_ref(dot3(au, sub3(pB, a0)), 0.0f, mag_a);
         pA = add3(a0, scale3(au, d));
     }
-    dist = len3(sub3(pA, pB));
+    dist = SQ ? lensq3(sub3(pA, pB)) : len3(sub3(pA, pB));
     if (WANT_S) s_out = sb;
     return true;
+}
+
+// The correctly rounded float square root without the small-input scaling of the compiler's
+// expansion: v_sqrt_f32 (within 1 ulp) and the same +-1 ulp residual correction, in the same order.
+// For x >= 2^-96 the compiler's sequence takes exactly these steps, so the result is bit-identical
+// to sqrtf(x) there; also for 0, +inf and NaN (as NaN).  Below 2^-96 (the compiler scales by 2^32
+// first) the result may differ in the last bits: callers use it only where such inputs cannot occur
+// or cannot change a result.
+__device__ __forceinline__ float sqrt_cr_noscale(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1);
+    const float sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    const float r = (rm <= 0.0f) ? sm : s;
+    return (rp > 0.0f) ? sp : r;
 }
 
 __host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu, float mag_b,
