@@ -874,11 +874,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     const int discard = kQueueCap + lane;
     const auto push = [&](unsigned long long m, int32_t e_beam, int32_t e_lane) {
         if (m == 0ull) return;
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
-        // slot = lane in m ? rank : discard, as one v_cndmask on the scalar mask (every lane stores)
-        int slot;
-        asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(slot) : "v"(discard), "v"(rank), "s"(m));
+        int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
+        // computed by every lane (an opaque use keeps the compiler from sinking it under an exec mask),
+        // then slot = lane in m ? rank : discard with the scalar mask itself as the select's condition
+        // (inverse ballot): one v_cndmask, every lane stores
+        asm volatile("" : "+v"(rank));
+        const int slot = __builtin_amdgcn_inverse_ballot_w64(m) ? rank : discard;
         sh.q[slot] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
         if (COUNT) pf.queued += __popcll(m);
