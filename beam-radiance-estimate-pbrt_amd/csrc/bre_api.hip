@@ -450,6 +450,9 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     const bool want_cnt = c->counters || seg_counts;
     const size_t per_seg = (size_t)c->split * (12 + (want_cnt ? 8 : 0));
     int64_t chunk = c->partial_cap / (int64_t)per_seg / 64 * 64;
+    // the exact stage addresses a launch's SegRec records with 32-bit byte offsets (BRE_BUF_LOADS):
+    // at most 2^26 segments (64 B each) per launch
+    if (chunk > ((int64_t)1 << 26)) chunk = (int64_t)1 << 26;
     if (chunk < 64) chunk = 64;
     if (chunk > nseg) chunk = nseg;
     HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));

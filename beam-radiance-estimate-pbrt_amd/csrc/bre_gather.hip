@@ -79,9 +79,9 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_SQRT_NOSCALE
 #define BRE_SQRT_NOSCALE 1
 #endif
-// BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes and the power through buffer
-// descriptors (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer
-// math; C2 +0.8%, C3 +2%, profiles/r3b/run4)
+// BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes through a buffer descriptor
+// (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer math;
+// with the power too, C2 +0.8%, C3 +2%, profiles/r3b/run4)
 #ifndef BRE_BUF_LOADS
 #define BRE_BUF_LOADS 1
 #endif
@@ -702,12 +702,15 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
 #elif BRE_BUF_LOADS
     (void)L;
     (void)sr;
-    // SegRec plane k of this packet at byte (seg0 / 64) * 4096 + k * 1024 + sl * 16 (packet-plane layout)
-    const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec), prs = buf_rsrc(pw);
+    // SegRec plane k of this packet at byte (seg0 / 64) * 4096 + k * 1024 + sl * 16 (packet-plane layout;
+    // one launch's records stay far below 4 GiB: bre_api.hip caps a launch's segments).  The beam
+    // record and power stay 64-bit pointer loads: a beam index may exceed 2^26 (2^28) records of 64
+    // (16) bytes, past a 32-bit byte offset.
+    const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec);
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
     const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
     const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
-    const float4 pv = buf_f4(prs, (unsigned int)b << 4, 0u);
+    const float4 pv = pw[b];
 #else
     (void)L;
     const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
