@@ -64,6 +64,7 @@ struct bre_ctx {
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
+    int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
     int tile_axis = 0;       // internal: tile kernel tile axis reject (GatherArgs::tileax), 1 = on (measured slower)
     int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
@@ -87,6 +88,7 @@ struct bre_ctx {
     DevMem sp_o, sp_p, sp_d, sp_t, sp_pix, sp_index;  // this packet shard's segments (contiguous)
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
+    BeamSet bset;  // the built set's radius layout (BeamRec)
     int built_leaf_size = 1;
     DevMem in_start, in_end, in_radius, in_power;  // staging for host-pointer uploads
     DevMem box, cent, cbounds, nvalid_buf, keys, keys_alt, vals, vals_alt, sort_tmp, leaf_parent, visit, gbox;
@@ -142,6 +144,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
                  const float *power) {
     c->nbeams = n;
     c->nvalid = 0;
+    c->bset = BeamSet{};
     c->nnodes = 0;
     c->roots_split = -1;
     c->stats = bre_stats{};
@@ -154,7 +157,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     HIPCHK(c, c->box.ensure(N * 6 * sizeof(float)));
     HIPCHK(c, c->cent.ensure(N * 3 * sizeof(float)));
     HIPCHK(c, c->cbounds.ensure(12 * sizeof(unsigned int)));
-    HIPCHK(c, c->nvalid_buf.ensure(sizeof(unsigned int)));
+    HIPCHK(c, c->nvalid_buf.ensure(3 * sizeof(unsigned int)));
     HIPCHK(c, c->keys.ensure(N * sizeof(unsigned long long)));
     HIPCHK(c, c->keys_alt.ensure(N * sizeof(unsigned long long)));
     HIPCHK(c, c->vals.ensure(N * sizeof(int32_t)));
@@ -184,11 +187,16 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     HIPCHK(c, launch_prep(b, c->stream));
     HIPCHK(c, launch_morton(b, c->stream));
     HIPCHK(c, launch_sort(b, c->stream));
-    unsigned int nv = 0;
-    HIPCHK(c, hipMemcpyAsync(&nv, b.nvalid, sizeof(nv), hipMemcpyDeviceToHost, c->stream));
+    unsigned int nv[3] = {0u, 0u, 0u};  // valid beams, min / max of their radius bits (k_prep)
+    HIPCHK(c, hipMemcpyAsync(nv, b.nvalid, sizeof(nv), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int64_t nvalid = nv;
+    const int64_t nvalid = nv[0];
     c->nvalid = nvalid;
+    // one radius for every valid beam: the records carry the power instead (BeamRec, BeamSet)
+    c->bset.uniform = (nvalid > 0 && nv[1] == nv[2] && !c->split_records) ? 1 : 0;
+    std::memcpy(&c->bset.radius, &nv[1], sizeof(float));
+    if (!c->bset.uniform) c->bset.radius = 0.f;
+    b.uniform_radius = c->bset.uniform;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
     if (c->kernel == 0 && c->beam_key >= 1) {
@@ -251,6 +259,7 @@ bre_status gather_chunk(bre_ctx *c, const GatherArgs &a) {
     const size_t st = chunk_scan_temp_bytes(np);
     HIPCHK(c, c->ch_scan_tmp.ensure(st + 16));
     cb.parents = c->recs.as<BeamRec>();
+    cb.bset = c->bset;
     cb.nparents = np;
     cb.seg_o = a.o;
     cb.seg_p = a.p;
@@ -412,6 +421,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.seg_index = seg_index;
     a.recs = c->recs.as<BeamRec>();
     a.pow = c->pow.as<float4>();
+    a.bset = c->bset;
     a.nodes = c->nodes.as<Node>();
     a.nvalid = c->nvalid;
     a.leaf_size = c->built_leaf_size;
@@ -675,6 +685,11 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 112:  // internal: tile kernel tile axis reject, 1 on / 0 off (default; A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0 or 1");
         c->tile_axis = (int)value;
+        return BRE_OK;
+    case 113:  // internal: beam record layout, 0 power in the record for uniform-radius sets (default)
+               // / 1 always radius in the record, power apart (A/B; applies from the next build)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "record layout must be 0 or 1");
+        c->split_records = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");

@@ -61,18 +61,20 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
                                                  const float *__restrict__ radius, int64_t n, int sqrt_mode,
                                                  float *__restrict__ box, float *__restrict__ cent,
                                                  unsigned int *__restrict__ cbounds, unsigned int *__restrict__ nvalid) {
-    __shared__ unsigned int red[kBlock / 64][13];
+    __shared__ unsigned int red[kBlock / 64][15];
     // ordered-uint min (lo) / max (hi) of valid centroids and of valid beams' end points; identity values
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
     unsigned int mx[3] = {0u, 0u, 0u};
     unsigned int emn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
     unsigned int emx[3] = {0u, 0u, 0u};
     unsigned int cnt = 0;
+    unsigned int rmn = 0xffffffffu, rmx = 0u;  // min / max of the valid beams' radius bits
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         const f3 s = mk(start[3 * i], start[3 * i + 1], start[3 * i + 2]);
         const f3 e = mk(end[3 * i], end[3 * i + 1], end[3 * i + 2]);
+        const float rad = radius[i];
         f3 lo, hi;
-        world_bound(s, e, radius[i], sqrt_mode, lo, hi);
+        world_bound(s, e, rad, sqrt_mode, lo, hi);
         float b[6] = {lo.x, lo.y, lo.z, hi.x, hi.y, hi.z};
 #pragma unroll
         for (int k = 0; k < 6; ++k) box[6 * i + k] = b[k];
@@ -93,6 +95,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
                 emn[k] = min(emn[k], min(us[k], ue[k]));
                 emx[k] = max(emx[k], max(us[k], ue[k]));
             }
+            rmn = min(rmn, __float_as_uint(rad));
+            rmx = max(rmx, __float_as_uint(rad));
             ++cnt;
         }
     }
@@ -107,6 +111,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
             emx[k] = max(emx[k], (unsigned int)__shfl_xor((int)emx[k], off));
         }
         cnt += (unsigned int)__shfl_xor((int)cnt, off);
+        rmn = min(rmn, (unsigned int)__shfl_xor((int)rmn, off));
+        rmx = max(rmx, (unsigned int)__shfl_xor((int)rmx, off));
     }
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -118,6 +124,8 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
             red[w][10 + k] = emx[k];
         }
         red[w][6] = cnt;
+        red[w][13] = rmn;
+        red[w][14] = rmx;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -130,9 +138,13 @@ __global__ __launch_bounds__(kBlock) void k_prep(const float *__restrict__ start
                 emx[k] = max(emx[k], red[v][10 + k]);
             }
             cnt += red[v][6];
+            rmn = min(rmn, red[v][13]);
+            rmx = max(rmx, red[v][14]);
         }
         if (cnt != 0u) {
             atomicAdd(nvalid, cnt);
+            atomicMin(&nvalid[1], rmn);
+            atomicMax(&nvalid[2], rmx);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 atomicMin(&cbounds[k], mn[k]);
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
                                                  const unsigned long long *__restrict__ keys,
                                                  const int32_t *__restrict__ vals, int64_t nvalid,
                                                  const float *__restrict__ gbox, BeamRec *__restrict__ recs,
-                                                 float4 *__restrict__ pw) {
+                                                 float4 *__restrict__ pw, int uniform_radius) {
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= nvalid) return;
     const int32_t i = vals[s];
@@ -314,13 +326,15 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
     r.b0[0] = b0.x; r.b0[1] = b0.y; r.b0[2] = b0.z;
     r.bu[0] = bu.x; r.bu[1] = bu.y; r.bu[2] = bu.z;
     r.mag_b = magB;
-    r.radius = radius[i];
-    r.pad[0] = 0.0f;
-    r.pad[1] = 0.0f;
-    recs[s] = r;
     // `1e-5 * beam->powerEnd` = powerEnd.c[k] * (Float)1e-5  (photonbeam.cpp:504, spectrum.h:165-179)
     const float k5 = 1e-5f;
-    pw[s] = make_float4(power[3 * i] * k5, power[3 * i + 1] * k5, power[3 * i + 2] * k5, 0.0f);
+    const float4 p = make_float4(power[3 * i] * k5, power[3 * i + 1] * k5, power[3 * i + 2] * k5, 0.0f);
+    // a uniform-radius set carries the power in the record (BeamRec, BeamSet)
+    r.radius = uniform_radius ? p.x : radius[i];
+    r.pad[0] = uniform_radius ? p.y : 0.0f;
+    r.pad[1] = uniform_radius ? p.z : 0.0f;
+    recs[s] = r;
+    pw[s] = p;
 }
 
 __device__ __forceinline__ int ldelta(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf, int i, int j) {
@@ -458,7 +472,11 @@ hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(b.cbounds + 9, 0, 3 * sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.nvalid, 0, sizeof(unsigned int), s);
+    e = hipMemsetAsync(b.nvalid, 0, sizeof(unsigned int), s);  // valid count
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.nvalid + 1, 0xff, sizeof(unsigned int), s);  // radius bits min
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(b.nvalid + 2, 0, sizeof(unsigned int), s);  // radius bits max
     if (e != hipSuccess) return e;
     if (b.n == 0) return hipSuccess;
     const unsigned prep_grid = (unsigned)std::min<int64_t>((int64_t)grid_for(b.n), 2048);  // grid-stride
@@ -502,7 +520,8 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s) {
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (nvalid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power, b.box,
-                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key >= 1 ? b.gbox : nullptr, b.recs, b.pow);
+                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key >= 1 ? b.gbox : nullptr, b.recs, b.pow,
+                       b.uniform_radius);
     return hipGetLastError();
 }
 

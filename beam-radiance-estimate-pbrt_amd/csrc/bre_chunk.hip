@@ -150,7 +150,7 @@ __device__ __forceinline__ bool parent_usable(const BeamRec &r) {
     return ok;
 }
 
-__global__ __launch_bounds__(kBlock) void k_chunk_count(const BeamRec *__restrict__ parents, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_chunk_count(const BeamRec *__restrict__ parents, BeamSet bset, int64_t n,
                                                         const unsigned int *__restrict__ seg_bounds, float R,
                                                         float len_factor, int32_t *__restrict__ counts,
                                                         float *__restrict__ range) {
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_count(const BeamRec *__restric
     float t_in = 0.f, t_out = 0.f;
     if (parent_usable(r) && seg_bounds[0] <= seg_bounds[3]) {
         const Clip c = load_clip(seg_bounds);
-        const float E = chunk_E(R, r.radius, c.margin);
+        const float E = chunk_E(R, beam_radius(bset, r.radius), c.margin);
         const f3 lo = mk(c.lo.x - E, c.lo.y - E, c.lo.z - E), hi = mk(c.hi.x + E, c.hi.y + E, c.hi.z + E);
         const f3 b0 = mk(r.b0[0], r.b0[1], r.b0[2]), bu = mk(r.bu[0], r.bu[1], r.bu[2]);
         if (isfinite(E) && E > 0.f && clip_line(b0, bu, lo, hi, t_in, t_out)) {
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_count(const BeamRec *__restric
     range[2 * i + 1] = t_out;
 }
 
-__global__ __launch_bounds__(kBlock) void k_chunk_emit(const BeamRec *__restrict__ parents, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_chunk_emit(const BeamRec *__restrict__ parents, BeamSet bset, int64_t n,
                                                        const unsigned int *__restrict__ seg_bounds, float R,
                                                        const int32_t *__restrict__ counts,
                                                        const int64_t *__restrict__ offsets,
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_emit(const BeamRec *__restrict
     if (cnt > 0) {
         const BeamRec r = parents[i];
         const Clip c = load_clip(seg_bounds);
-        const float E = chunk_E(R, r.radius, c.margin);
+        const float E = chunk_E(R, beam_radius(bset, r.radius), c.margin);
         const f3 b0 = mk(r.b0[0], r.b0[1], r.b0[2]), bu = mk(r.bu[0], r.bu[1], r.bu[2]);
         const float t_in = range[2 * i], t_out = range[2 * i + 1];
         const float span = t_out - t_in, fn = (float)cnt;
@@ -220,7 +220,8 @@ __global__ __launch_bounds__(kBlock) void k_chunk_emit(const BeamRec *__restrict
     wave_minmax_atomic(mn, mx, cnt > 0, cbounds);
 }
 
-__global__ __launch_bounds__(kBlock) void k_chunk_pack(const BeamRec *__restrict__ parents, int64_t nchunks,
+__global__ __launch_bounds__(kBlock) void k_chunk_pack(const BeamRec *__restrict__ parents, BeamSet bset,
+                                                       int64_t nchunks,
                                                        const int32_t *__restrict__ order,
                                                        const float *__restrict__ box, const float *__restrict__ s_lo,
                                                        const float *__restrict__ s_hi,
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_pack(const BeamRec *__restrict
         q.bu[k] = r.bu[k];
     }
     q.mag_b = r.mag_b;
-    q.radius = r.radius;
+    q.radius = beam_radius(bset, r.radius);
     q.s_lo = s_lo[c];
     q.s_hi = s_hi[c];
     out[j] = q;
@@ -440,7 +441,7 @@ hipError_t launch_chunk_count(const ChunkBuild &c, hipStream_t s) {
                            c.seg_bounds);
     if (c.nparents > 0)
         hipLaunchKernelGGL(k_chunk_count, dim3(grid_of(c.nparents, kBlock)), dim3(kBlock), 0, s, c.parents,
-                           c.nparents, c.seg_bounds, c.R, c.len_factor, c.counts, c.range);
+                           c.bset, c.nparents, c.seg_bounds, c.R, c.len_factor, c.counts, c.range);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(c.offsets, 0, sizeof(int64_t), s);
@@ -453,8 +454,8 @@ hipError_t launch_chunk_count(const ChunkBuild &c, hipStream_t s) {
 hipError_t launch_chunk_emit(const ChunkBuild &c, float *box, float *cent, float *s_lo, float *s_hi,
                              int32_t *parent, hipStream_t s) {
     if (c.nparents == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_chunk_emit, dim3(grid_of(c.nparents, kBlock)), dim3(kBlock), 0, s, c.parents, c.nparents,
-                       c.seg_bounds, c.R, c.counts, c.offsets, c.range, box, cent, s_lo, s_hi, parent, c.cbounds);
+    hipLaunchKernelGGL(k_chunk_emit, dim3(grid_of(c.nparents, kBlock)), dim3(kBlock), 0, s, c.parents, c.bset,
+                       c.nparents, c.seg_bounds, c.R, c.counts, c.offsets, c.range, box, cent, s_lo, s_hi, parent, c.cbounds);
     return hipGetLastError();
 }
 
@@ -462,7 +463,8 @@ hipError_t launch_chunk_pack(const ChunkBuild &c, int64_t nchunks, const int32_t
                              const float *s_lo, const float *s_hi, const int32_t *parent, ChunkRec *out,
                              int32_t *out_parent, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_chunk_pack, dim3(grid_of(nchunks, kBlock)), dim3(kBlock), 0, s, c.parents, nchunks, order,
+    hipLaunchKernelGGL(k_chunk_pack, dim3(grid_of(nchunks, kBlock)), dim3(kBlock), 0, s, c.parents, c.bset, nchunks,
+                       order,
                        box, s_lo, s_hi, parent, out, out_parent);
     return hipGetLastError();
 }

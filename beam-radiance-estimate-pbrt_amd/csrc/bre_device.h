@@ -6,17 +6,28 @@
 
 namespace bre {
 
-// One beam in BVH (sorted) order: 64 B, one cache line.  Everything the per-pair test needs
-// except the power, which is only read when a pair contributes.
+// One beam in BVH (sorted) order: 64 B, one cache line.  Everything the per-pair test needs.
+// When every valid beam of the set has the same radius (BeamSet::uniform: the integrator's own beams
+// always do, photonbeam.cpp:292 stores the pass radius in each), the radius is the set's and the last
+// three words hold the beam's scaled power (the float4 power array's x, y, z), so a contributing pair
+// reads one record instead of a record and a power line.
 struct alignas(16) BeamRec {
     float lo[3], hi[3];  // reference test box: WorldBound, or the union over beams with an
                          // identical centroid (those share one SAH leaf in the reference)
     float b0[3];         // beam start
     float bu[3];         // (end - start) * (1/|end - start|)
     float mag_b;         // |end - start|
-    float radius;        // beam radius (PhotonBeam::radius)
-    float pad[2];
+    float radius;        // beam radius (PhotonBeam::radius); uniform sets: power.x
+    float pad[2];        // uniform sets: power.y, power.z
 };
+// How a gather reads a BeamRec's radius and power (the build's finding, passed by value).
+struct BeamSet {
+    int uniform = 0;      // 1: every valid beam has radius `radius`, power in the record's last words
+    float radius = 0.f;
+};
+__device__ __forceinline__ float beam_radius(const BeamSet &u, float rec_radius) {
+    return u.uniform ? u.radius : rec_radius;
+}
 static_assert(sizeof(BeamRec) == 64, "BeamRec must be one 64-B line");
 
 // Binary BVH interior node, 64 B: both children's boxes live in the parent so one line per
@@ -69,7 +80,8 @@ struct BuildBuffers {
     float *cent;       // 3n (input order)
     unsigned int *cbounds;  // 12 ordered uints: min/max of valid centroids, then of their end points
     float *gbox;            // 6n (input order): equal-centroid group boxes (tree key 1)
-    unsigned int *nvalid;   // 1
+    unsigned int *nvalid;   // 3: valid beams, then the ordered min and max of their radii
+    int uniform_radius = 0; // k_pack: the set's BeamSet::uniform (read back after k_prep)
     unsigned long long *keys, *keys_alt;
     int32_t *vals, *vals_alt;
     void *sort_tmp;
@@ -145,6 +157,7 @@ struct GatherArgs {
     const int32_t *seg_index;  // may be null: seg_rgb / seg_counts entry of gathered segment s is seg_index[s]
     const BeamRec *recs;
     const float4 *pow;
+    BeamSet bset;
     const Node *nodes;
     int64_t nvalid;
     int leaf_size;
@@ -168,6 +181,7 @@ struct GatherArgs {
 // capsule-chunk index (bre_chunk.hip)
 struct ChunkBuild {
     const BeamRec *parents;   // sorted parent beam records (reference group boxes)
+    BeamSet bset;
     int64_t nparents;
     const float *seg_o, *seg_p;  // the gather's segments (clip box)
     int64_t nseg;

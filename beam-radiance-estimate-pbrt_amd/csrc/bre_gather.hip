@@ -406,7 +406,8 @@ __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__res
 
 // One wave per leaf tile: axis = mean start -> mean end of its usable beams, rho = the largest
 // distance of a clipped beam line's end points from the axis (with rounding margins).
-__global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ recs, int64_t nvalid, int leaf_size,
+__global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ recs, BeamSet bset, int64_t nvalid,
+                                                  int leaf_size,
                                                   const unsigned int *__restrict__ segb, float R,
                                                   TileAxis *__restrict__ out) {
     const int64_t tile = blockIdx.x;
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
     f3 b0 = mk(0.f, 0.f, 0.f), bu = mk(0.f, 0.f, 0.f);
     float mb = 0.f, rad = 0.f;
     if (ok) {
-        const BeamV r = load_beam(recs, j);
+        const BeamV r = load_beam(recs, j, bset);
         b0 = r.b0;
         bu = r.bu;
         mb = r.mag_b;
@@ -672,7 +673,8 @@ struct TileShared {
 // The pair's segment comes from its SegRec, the beam line from L2.
 __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
                                            const float *__restrict__ sd, int64_t seg0,
-                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, float R,
+                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                           const BeamSet &bset, float R,
                                            bool count, const Lane &L) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
@@ -690,7 +692,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const int sa = sl << 2;
     const auto shf = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(v))); };
     const float4 s1 = sr[64], bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
-    const float4 pv = pw[b];
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
     const float4 s0 = make_float4(shf(L.o.x), shf(L.o.y), shf(L.o.z), shf(L.tmax));
     const float4 s3 = make_float4(shf(L.invs.x), shf(L.invs.y), shf(L.invs.z), 0.f);
 #if BRE_EXACT_SHFL == 2
@@ -710,12 +712,13 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
     const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
     const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
-    const float4 pv = pw[b];
+    // a uniform-radius set's power is in the record's last three words (BeamRec): eight loads per pair
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
 #else
     (void)L;
     const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
     const float4 s1 = sr[64], s2 = sr[128], bz = rb[2], bw = rb[3];
-    const float4 pv = pw[b];
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
 #endif
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
@@ -738,7 +741,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     float4 v = make_float4(0.f, 0.f, 0.f, 1.f);
     bool contrib = false;
     if (hit) {
-        const float maxd = R + bw.y;  // MaxDistance = currentBeamRadius + beam->radius
+        const float maxd = R + beam_radius(bset, bw.y);  // MaxDistance = currentBeamRadius + beam->radius
         float d2, unused;
         const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w,
                                                         mk(by.z, by.w, bz.x), mk(bz.y, bz.z, bz.w), bw.x, d2, unused);
@@ -814,7 +817,7 @@ template <bool COUNT, int MINW>
 __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
-    int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+    int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, BeamSet bset,
     const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
     DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan, int margin,
     const TileAxis *__restrict__ tax) {
@@ -898,7 +901,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         int h = 0;
         while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, R, count_c, L);
+            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, count_c, L);
             h += 64;
             __builtin_amdgcn_wave_barrier();
         }
@@ -938,7 +941,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         T.ab = 0.f;
         bool keep = false;
         if (lane < nb) {
-            const BeamV r = load_beam(recs, first + lane);
+            const BeamV r = load_beam(recs, first + lane, bset);
             T = make_scan_beam(r, R, margin);
             // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
             // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
@@ -966,7 +969,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 const bool kept = (km >> j) & 1ull;
                 const unsigned long long mk_ = scan_keep_mask(SL, L.au, scan_beam_lds(sh.tile, j)) & onm;
                 const bool need = kept && ((mk_ >> lane) & 1ull);
-                const Box6 box = load_beam(recs, first + j).box;
+                const Box6 box = load_beam(recs, first + j, bset).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                 if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
@@ -1144,7 +1147,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, R, count_c, L);
+            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, bset, R, count_c, L);
         }
         t1 = 0;
     }
@@ -1342,8 +1345,8 @@ __global__ __launch_bounds__(kThreadBlock) void k_gather_thread(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, const int32_t *__restrict__ pixel, float R, int64_t npix,
     float *__restrict__ accum, float *__restrict__ seg_rgb, int32_t *__restrict__ seg_counts,
-    const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, const Node *__restrict__ nodes, int64_t nvalid,
-    int leaf_size, DevCounters *ctr, int stack_cap) {
+    const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, BeamSet bset, const Node *__restrict__ nodes,
+    int64_t nvalid, int leaf_size, DevCounters *ctr, int stack_cap) {
     __shared__ int32_t stk[kThreadStackDepth][kThreadBlock];
     const int tid = threadIdx.x;
     const int64_t s = (int64_t)blockIdx.x * kThreadBlock + tid;
@@ -1367,14 +1370,14 @@ __global__ __launch_bounds__(kThreadBlock) void k_gather_thread(
                 const int64_t first = (int64_t)(~c0) * leaf_size;
                 const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
                 for (int j = 0; j < cnt; ++j)
-                    eval_beam<COUNT>(L, true, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand, contrib);
+                    eval_beam<COUNT>(L, true, load_beam(recs, first + j, bset), pw, first + j, R, cr, cg, cb, cand, contrib);
                 h0 = false;
             }
             if (h1 && c1 < 0) {
                 const int64_t first = (int64_t)(~c1) * leaf_size;
                 const int cnt = (int)min((int64_t)leaf_size, nvalid - first);
                 for (int j = 0; j < cnt; ++j)
-                    eval_beam<COUNT>(L, true, load_beam(recs, first + j), pw, first + j, R, cr, cg, cb, cand, contrib);
+                    eval_beam<COUNT>(L, true, load_beam(recs, first + j, bset), pw, first + j, R, cr, cg, cb, cand, contrib);
                 h1 = false;
             }
             if (h0 && h1) {
@@ -1434,11 +1437,11 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         if (a.seg_index && (a.seg_rgb || a.seg_counts)) return hipErrorInvalidValue;  // kernel 2 writes in place
         if (counters)
             hipLaunchKernelGGL(k_gather_thread<true>, grid, dim3(kThreadBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,
-                               a.pixel, a.R, a.npix, a.accum, rgb, cnt, a.recs, a.pow, a.nodes, a.nvalid,
+                               a.pixel, a.R, a.npix, a.accum, rgb, cnt, a.recs, a.pow, a.bset, a.nodes, a.nvalid,
                                a.leaf_size, a.ctr, stack_cap);
         else
             hipLaunchKernelGGL(k_gather_thread<false>, grid, dim3(kThreadBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,
-                               a.pixel, a.R, a.npix, a.accum, rgb, cnt, a.recs, a.pow, a.nodes, a.nvalid,
+                               a.pixel, a.R, a.npix, a.accum, rgb, cnt, a.recs, a.pow, a.bset, a.nodes, a.nvalid,
                                a.leaf_size, a.ctr, stack_cap);
         return hipGetLastError();
     }
@@ -1455,15 +1458,15 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         hipLaunchKernelGGL(k_segbox_init, dim3(1), dim3(64), 0, s, a.segbox);
         hipLaunchKernelGGL(k_segbox, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
                            a.segbox);
-        hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.nvalid, a.leaf_size,
-                           a.segbox, a.R, a.tileax);
+        hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.bset, a.nvalid,
+                           a.leaf_size, a.segbox, a.R, a.tileax);
         tax = a.tileax;
     }
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
-                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.nodes, a.nvalid, a.leaf_size, a.roots,    \
-                       a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin, tax)
+                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nvalid, a.leaf_size,     \
+                       a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin, tax)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

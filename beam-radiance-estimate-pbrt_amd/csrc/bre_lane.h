@@ -35,7 +35,7 @@ struct BeamV {
     float mag_b, radius;
     f3 pw;  // scaled powerEnd, when the caller already has it (kernel 3 batches)
 };
-__device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int64_t i) {
+__device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int64_t i, const BeamSet &bs) {
     const float4 *q = reinterpret_cast<const float4 *>(recs + i);
     const float4 x = q[0], y = q[1], z = q[2], w = q[3];
     BeamV r;
@@ -43,7 +43,7 @@ __device__ __forceinline__ BeamV load_beam(const BeamRec *__restrict__ recs, int
     r.b0 = mk(y.z, y.w, z.x);
     r.bu = mk(z.y, z.z, z.w);
     r.mag_b = w.x;
-    r.radius = w.y;
+    r.radius = beam_radius(bs, w.y);
     r.pw = mk(0.f, 0.f, 0.f);
     return r;
 }

@@ -92,6 +92,7 @@ def parse(argv=None):
     ap.add_argument("--beam-key", type=int, default=-1, help=argparse.SUPPRESS)  # tree build key study (option 110)
     ap.add_argument("--margin", type=int, default=-1, help=argparse.SUPPRESS)  # prefilter margin A/B (option 111)
     ap.add_argument("--tile-axis", type=int, default=-1, help=argparse.SUPPRESS)  # tile axis reject A/B (option 112)
+    ap.add_argument("--split-records", type=int, default=-1, help=argparse.SUPPRESS)  # BeamRec layout A/B (option 113)
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
@@ -221,6 +222,8 @@ def main():
             c.set_option(111, args.margin)
         if args.tile_axis >= 0:
             c.set_option(112, args.tile_axis)
+        if args.split_records >= 0:
+            c.set_option(113, args.split_records)
         # one explicit stream per context, shared with torch: the HIP events that time the gather
         # kernel are recorded on the stream the kernel runs on
         st = torch.cuda.Stream(dev)
