@@ -34,9 +34,13 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
     st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000, "queued_pairs": 500}
     r = bench.roofline(st, a, WL(), 2.0, None, None)
     items = (640 + 63) // 64 * 4
-    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 144.0 * 500 + 640 * 12 * (4 + 1)
+    # 128 B per queued pair: the uniform-radius record carries the power (144 B with the split layout)
+    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 128.0 * 500 + 640 * 12 * (4 + 1)
     # without the PMC passes: the HBM roofline of the algorithmic bytes
     assert r["bound"] == "hbm" and r["hbm"]["algorithmic_bytes_per_launch"] == alg
+    a_split = bench.parse(["--split", "4", "--split-records", "1"])
+    r_split = bench.roofline(st, a_split, WL(), 2.0, None, None)
+    assert r_split["hbm"]["algorithmic_bytes_per_launch"] == alg + 16.0 * 500
     assert r["achieved"] == pytest.approx(alg / 2e-3 / 1e9)
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and r["unit"] == "GB/s" and r["traffic"] is None
     # with them: VALU issue binds; frac = instructions / (256 CU x 4 SIMD / 2 x clocks), HBM kept aside
