@@ -674,7 +674,7 @@ struct TileShared {
 __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
                                            const float *__restrict__ sd, int64_t seg0,
                                            const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
-                                           const BeamSet &bset, float R,
+                                           const BeamSet &bset, float R, float inv_maxd,
                                            bool count, const Lane &L) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
@@ -754,7 +754,14 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
         const float dist = sqrtf(d2);
 #endif
         if (ok & (dist < maxd)) {
-            const float rr = dist / maxd;
+            // r = dist / MaxDistance.  A uniform-radius set shares MaxDistance = R + radius over the
+            // gather: the correctly rounded quotient from its reciprocal (div_by_shared, bit-identical to
+            // the division; a quotient below 2^-126 gives r^2 = 0 and w = 1 either way)
+            float rr;
+            if (bset.uniform)
+                rr = div_by_shared(dist, maxd, inv_maxd);
+            else
+                rr = dist / maxd;
             // 1 - fl(r^2) is 0 or >= 2^-24 (fl(r^2) <= 1 - 2^-24 unless it is 1): never in the scaled range
 #if BRE_SQRT_NOSCALE
             const float w = sqrt_cr_noscale(1.0f - rr * rr);
@@ -862,6 +869,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     // the largest lane margin Al' of the packet, folded into every beam's threshold at staging (a
     // zero-length segment, Al' = FLT_MAX, is never rejected anyway: see scan_need)
     const float al_max = uniform_f(wave_max(valid && SL.al < FLT_MAX ? SL.al : 0.f));
+    // 1 / MaxDistance of a uniform-radius set, correctly rounded, once per wave (tile_exact)
+    const float inv_maxd = bset.uniform ? uniform_f(1.0f / (R + bset.radius)) : 0.f;
     sh.acc[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     __builtin_amdgcn_wave_barrier();
     int cand = 0;
@@ -901,7 +910,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         int h = 0;
         while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, count_c, L);
+            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
             h += 64;
             __builtin_amdgcn_wave_barrier();
         }
@@ -1147,7 +1156,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, bset, R, count_c, L);
+            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
         }
         t1 = 0;
     }

@@ -199,6 +199,21 @@ __device__ __forceinline__ float sqrt_cr_noscale(float x) {
     return (rp > 0.0f) ? sp : r;
 }
 
+// a / b correctly rounded for a divisor b shared by many divisions, given y = 1 / b correctly rounded
+// (computed once): q0 = a y, then two Markstein corrections r = a - b q (exact by FMA), q + r y.  After
+// the first, q is a faithful quotient; with y within half an ulp of 1 / b, the second then returns
+// RN(a / b) (Markstein's theorem; Muller et al., Handbook of Floating-Point Arithmetic, the division
+// chapter), barring underflow / overflow.  Five VALU instead of the general expansion's ten plus its
+// scaling steps.  Callers: a, b finite, b > 0, a / b not below the normal range or where such a
+// quotient cannot change the result.
+__device__ __forceinline__ float div_by_shared(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r0 = __builtin_fmaf(-q0, b, a);
+    const float q1 = __builtin_fmaf(r0, y, q0);
+    const float r1 = __builtin_fmaf(-q1, b, a);
+    return __builtin_fmaf(r1, y, q1);
+}
+
 __host__ __device__ __forceinline__ bool closest_distance(f3 a0, f3 a1, f3 au, float mag_a, f3 b0, f3 bu, float mag_b,
                                                           float &dist) {
     float unused;

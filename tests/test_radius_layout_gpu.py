@@ -6,7 +6,8 @@ reads the radius from the set (BeamSet); otherwise the record keeps its radius a
 from its own array (bre_device.h BeamRec).  The integrator's beams always share the pass radius
 (photonbeam.cpp:292), so the other tests run the uniform layout; these run mixed radii (one outlier
 beam, and radii drawn per beam) through every kernel against the oracle, and check that the two
-layouts give bit-identical sums on the same uniform set."""
+layouts give bit-identical sums on the same uniform set (the uniform layout also divides by the
+shared MaxDistance through its reciprocal, bre_math.h div_by_shared)."""
 import numpy as np
 import pytest
 
@@ -76,3 +77,28 @@ def test_uniform_and_split_layouts_bit_identical(bre, synth):
     assert res[0]["counts"][:, 1].sum() > 1000
     assert np.array_equal(res[0]["counts"], res[1]["counts"])
     assert np.array_equal(res[0]["seg_rgb"].view(np.uint32), res[1]["seg_rgb"].view(np.uint32))
+
+
+@pytest.mark.parametrize("iteration", [0, 12])
+def test_layouts_bit_identical_on_c2(bre, scene_mod_gpu, iteration):
+    """The same on real C2 data (millions of contributing pairs): the uniform layout also divides by
+    the set's MaxDistance through its reciprocal (bre_math.h div_by_shared), which must give the
+    correctly rounded quotient of every pair, as the split layout's division does."""
+    import torch
+
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+    R = bre.beam_radius_at(0.01, 0.5, iteration)
+    out = {}
+    for split in (0, 1):
+        with bre.BeamGather(0) as g:
+            g.set_option(113, split)
+            g.trace_photons(scene, 300_000, iteration, 5, R)
+            n = g.camera_pass(scene, 256, 256, iteration, 5, True, True)
+            rgb = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+            cnt = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
+            g.gather_camera_segments(R, seg_rgb=rgb, counts=cnt)
+            g.synchronize()
+            out[split] = (rgb.cpu().numpy(), cnt.cpu().numpy())
+    assert out[0][1][:, 1].sum() > 1_000_000
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
