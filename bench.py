@@ -24,9 +24,11 @@ pixel bands.  `--scaling weak` gives every rank its own film of the same size (N
 `--emulate-shard R/N` runs rank R's share of an N-GPU strong-scaling run alone on one GPU.
 
 Also reported (rank 0, N = 1):
-* `roofline` — the tile kernel's binding unit, VALU issue (`bound` "valu_issue"): wave64 VALU
+* `roofline` — the tile kernel's VALU issue roofline (`bound` "valu_issue"): wave64 VALU
   instructions per second of the iteration-0 launch against 256 CU x 4 SIMD / 2 clocks, from this
-  run's own rocprofv3 PMC passes (`issue`: SQ counters, LDS busy, waits); `traffic` = HBM bytes per
+  run's own rocprofv3 PMC passes (`issue`: SQ counters, LDS busy, waits, and the vector-memory
+  path's TA / TD busy fractions with the busiest unit named -- since round 3 the TD data-return
+  path); `traffic` = HBM bytes per
   launch from the same passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE).  `hbm`: the
   algorithmic bytes per launch (node and beam lines of the visited tiles, the segments, the exact
   stage's 128 B per queued pair, the partial sums; counted live by the counter pass) / the launch's
@@ -360,7 +362,8 @@ def main():
 def roofline(st, args, wl, gather_ms, pmc, cpu):
     """Roofline of the tile kernel for one launch of iteration 0 (see the module docstring).
 
-    The binding unit is VALU issue: `achieved` = the launch's wave64 VALU instructions
+    The arithmetic roofline is VALU issue (`issue` also carries the TA / TD busy
+    fractions of the vector-memory path, the busiest unit since round 3): `achieved` = the launch's wave64 VALU instructions
     (SQ_INSTS_VALU) per second, `peak` = 256 CU x 4 SIMD x one wave64 instruction per 2 clocks at the
     clock the same counters measured, so `frac` = the VALU issue fraction.  The byte side is kept in
     `hbm`: the algorithmic bytes the packets request per launch against the 8 TB/s HBM peak (served
@@ -422,6 +425,8 @@ PMC_PASSES = {
     "write": ["WRITE_SIZE"],
     "sq": ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
            "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"],
+    # the vector-memory path: address (TA) and data-return (TD) units, one each per CU
+    "vmem": ["TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "SQ_INSTS_VMEM_RD"],
 }
 
 
@@ -487,8 +492,18 @@ def pmc_passes(args):
             "SQ_INSTS_VALU": vals["SQ_INSTS_VALU"], "SQ_INSTS_LDS": vals.get("SQ_INSTS_LDS"),
             "clocks": clocks,
             "model": "VALU peak = 256 CU x 4 SIMD-32 / 2 clocks per wave64 instruction; LDS busy = "
-                     "SQ_LDS_IDX_ACTIVE / (256 x clocks); clocks = GRBM_GUI_ACTIVE / 8 XCDs",
+                     "SQ_LDS_IDX_ACTIVE / (256 x clocks); TA / TD busy = TA_TA_BUSY_sum / TD_TD_BUSY_sum "
+                     "/ (256 x clocks); clocks = GRBM_GUI_ACTIVE / 8 XCDs",
         }
+        if "TD_TD_BUSY_sum" in vals:
+            iss = res["issue"]
+            iss["ta_busy_frac"] = vals.get("TA_TA_BUSY_sum", 0.0) / (CUS * clocks)
+            iss["td_busy_frac"] = vals["TD_TD_BUSY_sum"] / (CUS * clocks)
+            iss["SQ_INSTS_VMEM_RD"] = vals.get("SQ_INSTS_VMEM_RD")
+            # the busiest of the kernel's units (the TD data-return path)
+            units = {"valu_issue": iss["valu_issue_frac"], "lds": iss["lds_busy_frac"],
+                     "vmem_address_ta": iss["ta_busy_frac"], "vmem_data_td": iss["td_busy_frac"]}
+            iss["busiest_unit"] = max(units, key=units.get)
     return res
 
 
