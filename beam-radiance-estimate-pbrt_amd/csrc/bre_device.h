@@ -129,7 +129,8 @@ struct alignas(16) SegRec {
     float au[3];        // (p - o) * (1 / |p - o|)
     int32_t has_inf;    // some 1 / d_i is infinite (axis-parallel ray)
     float invs[3];      // 1 / d with infinities replaced by +-FLT_MAX
-    float omax;         // max |o_i| + |p - o|
+    int32_t has_inf3;   // has_inf again: the tile kernel's exact stage reads planes 0, 1 and 3 and
+                        // recomputes au from o, p and |A| (BRE_AU_RECOMPUTE)
 };
 static_assert(sizeof(SegRec) == 64, "SegRec must be one 64-B line");
 // plane k (0..3) of segment s in the packet-plane layout (buffers hold ceil(nseg / 64) * 64 records)

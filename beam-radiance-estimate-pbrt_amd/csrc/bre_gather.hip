@@ -39,6 +39,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
 // tiles not scanned), 5 = exact stage accumulates in one racy RMW round instead of the ordered rank
 // rounds (wrong sums: the price of the ordering).
+// Exact stage (buffer-load path): 1 = recompute the segment's unit direction instead of loading
+// SegRec plane 2 (default), 0 = load it (A/B)
+#ifndef BRE_AU_RECOMPUTE
+#define BRE_AU_RECOMPUTE 1
+#endif
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
 #endif
@@ -711,7 +716,16 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec);
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
     const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
+#if BRE_AU_RECOMPUTE
+    // au = (p - o) * (1 / |A|) by load_lane's own operations (bit-identical to plane 2, which is not
+    // loaded): VALU, which has headroom, for one of the pair's eight vector loads (the texture-data
+    // path is the kernel's busiest unit); has_inf from plane 3
+    const float4 s1 = buf_f4(srs, vo + 1024u, so_), bz = rb[2], bw = rb[3];
+    const f3 au_ = (s1.w != 0.0f) ? div3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s1.w) : mk(0.f, 0.f, 0.f);
+    const float4 s2 = make_float4(au_.x, au_.y, au_.z, s3.w);
+#else
     const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
+#endif
     // a uniform-radius set's power is in the record's last three words (BeamRec): eight loads per pair
     const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
 #else
@@ -1218,7 +1232,7 @@ __global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__r
     q[0] = make_float4(L.o.x, L.o.y, L.o.z, L.tmax);
     q[64] = make_float4(L.p.x, L.p.y, L.p.z, L.mag_a);
     q[128] = make_float4(L.au.x, L.au.y, L.au.z, __int_as_float(L.has_inf ? 1 : 0));
-    q[192] = make_float4(L.invs.x, L.invs.y, L.invs.z, L.omax);
+    q[192] = make_float4(L.invs.x, L.invs.y, L.invs.z, __int_as_float(L.has_inf ? 1 : 0));
 }
 
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the
