@@ -37,6 +37,7 @@ EXPORTS = [
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
     "bre_render_progressive", "bre_shard_segments", "bre_set_beams_sharded", "bre_gather_sharded",
+    "bre_device_check",
 ]
 
 
@@ -142,6 +143,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_set_beams_sharded.restype = I32
     lib.bre_gather_sharded.argtypes = [P, I32, I64, P, P, P, P, P, F, I64, P, P, P]
     lib.bre_gather_sharded.restype = I32
+    if hasattr(lib, "bre_device_check"):  # (absent from round-3 libraries loaded for A/B timing)
+        lib.bre_device_check.argtypes = [P, I32, I64, P, I32, P, P]
+        lib.bre_device_check.restype = I32
     _LIB = lib
     return lib
 
@@ -317,6 +321,19 @@ class BeamGather:
         n = tmax.shape[0]
         self._check(self.lib.bre_gather_device(self.h, n, _ptr(o), _ptr(p), _ptr(d), _ptr(tmax), _ptr(pixel),
                                                float(R), int(npix), _ptr(accum), _ptr(seg_rgb), _ptr(counts)))
+
+    def device_check(self, kind: int, x, aux=None):
+        """bre_device_check: libbre's device copies of NextFloatUp/Down (kinds 0/1), the exact
+        stage's square root next to sqrtf (2), FindInterval over aux (3) and the shared-reciprocal
+        division next to x / aux[0] (4).  Returns float32 [n] or [n, 2]."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[0]
+        two = kind in (2, 4)
+        y = np.zeros((n, 2) if two else n, np.float32)
+        a = None if aux is None else np.ascontiguousarray(aux, dtype=np.float32)
+        self._check(self.lib.bre_device_check(self.h, kind, n, _ptr(x), 0 if a is None else a.shape[0],
+                                              None if a is None else _ptr(a), _ptr(y)))
+        return y
 
     def close(self):
         if getattr(self, "h", None):

@@ -95,12 +95,14 @@ struct bre_ctx {
     DevMem recs, pow, nodes;
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
+    DevMem chk_x, chk_aux, chk_y;  // bre_device_check staging
     DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
     DevMem sc_tris, sc_nodes, sc_prims, sc_light_tri, sc_light_func, sc_light_cdf;
     uint64_t sc_hash = 0;  // hash of the uploaded triangles (0: none)
+    std::vector<unsigned char> sc_bytes;  // the uploaded triangles' bytes: a hash match is confirmed by memcmp
     DevScene sc_head;      // geometry fields of the uploaded scene
     // camera pass
     DevMem cam_dev, cam_perms, cs_o, cs_p, cs_d, cs_t, cs_pix, cs_valid, cam_offs, cam_tmp, cam_flags;
@@ -828,7 +830,12 @@ static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
         dd = c->grid_dens.as<float>();
     }
     const uint64_t h = hash_triangles(scene);
-    if (h != c->sc_hash) {
+    // the geometry is reused only when the hash AND the bytes match (a hash collision between two
+    // scenes must not trace against the stale BVH and lights)
+    const size_t tri_bytes = (size_t)scene->n_triangles * sizeof(bre_triangle);
+    const bool same = h == c->sc_hash && c->sc_bytes.size() == tri_bytes &&
+                      (tri_bytes == 0 || memcmp(c->sc_bytes.data(), scene_triangles(scene), tri_bytes) == 0);
+    if (!same) {
         HostScene hs;
         prepare_geometry(scene, &hs);
         if (hs.depth > kSceneStack)
@@ -854,6 +861,8 @@ static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
         c->sc_head.light_func = c->sc_light_func.as<float>();
         c->sc_head.light_cdf = c->sc_light_cdf.as<float>();
         c->sc_hash = h;
+        const unsigned char *tb = reinterpret_cast<const unsigned char *>(scene_triangles(scene));
+        c->sc_bytes.assign(tb, tb + tri_bytes);
     }
     DevScene ds = c->sc_head;
     prepare_medium(scene, &ds, dd);
@@ -1523,6 +1532,30 @@ int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int3
     const bool last = (nch - 1) % count == rank;                        // owns the only partial chunk
     const int64_t packets = q * K - (last ? nch * K - npk : 0);
     return packets * 64 - (last ? npk * 64 - n_segments : 0);
+}
+
+bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
+                            float *y) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (kind < 0 || kind > 4) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 4]", kind);
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: bad arrays");
+    const bool need_aux = kind >= 3;
+    if (need_aux && (n_aux < 1 || !aux)) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d needs aux", kind);
+    if (n == 0) return BRE_OK;
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    const int64_t outs = (kind == 2 || kind == 4) ? 2 * n : n;
+    HIPCHK(c, c->chk_x.ensure((size_t)n * 4));
+    HIPCHK(c, c->chk_y.ensure((size_t)outs * 4));
+    HIPCHK(c, c->chk_aux.ensure(need_aux ? (size_t)n_aux * 4 : 4));
+    HIPCHK(c, hipMemcpyAsync(c->chk_x.ptr, x, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    if (need_aux)
+        HIPCHK(c, hipMemcpyAsync(c->chk_aux.ptr, aux, (size_t)n_aux * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_device_check(kind, n, c->chk_x.as<float>(), need_aux ? n_aux : 0, c->chk_aux.as<float>(),
+                                  c->chk_y.as<float>(), c->stream));
+    HIPCHK(c, hipMemcpyAsync(y, c->chk_y.ptr, (size_t)outs * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BRE_OK;
 }
 
 float bre_beam_radius_at(float initial_radius, float alpha, int iteration) {

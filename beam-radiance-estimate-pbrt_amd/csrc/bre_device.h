@@ -248,6 +248,10 @@ hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chu
                               const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
                               float *p2, float *d2, float *t2, int32_t *pix2, int32_t *index2, hipStream_t st);
 
+// device self-check of the shared scalar primitives (bre_check.hip, bre_device_check)
+hipError_t launch_device_check(int kind, int64_t n, const float *x, int n_aux, const float *aux, float *y,
+                               hipStream_t s);
+
 // gather kernels (bre_gather.hip)
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);
 hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStream_t s);

@@ -912,7 +912,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const int slot = __builtin_amdgcn_inverse_ballot_w64(m) ? rank : discard;
         sh.q[slot] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
-        if (COUNT) pf.queued += __popcll(m);
+        if (count_c) pf.queued += __popcll(m);  // the production queue too, when counting contributions
         if (BRE_SCAN_STATS) ss_q += __popcll(m);
     };
     // run the exact stage on every full batch of 64 queued pairs (the one call site in the scan),
@@ -1033,7 +1033,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i), readlane_f(SL.q.z, i));
                 Si.al = 0.f;
                 const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i), readlane_f(L.au.z, i));
-                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tile, lane)), (int32_t)(cur_first + lane), i);
+                // & km: a beam the packet rejected (thr_sq = -inf) still passes scan_keep_mask when it
+                // is near-parallel to segment i (u < 0.0101); the beam-major scan never visits it
+                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tile, lane)) & km, (int32_t)(cur_first + lane), i);
                 drain();
             }
             if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
@@ -1186,6 +1188,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pcnt[2 * ((int64_t)sub * nseg + s) + 1] = (int32_t)a.w;
         }
     }
+    // the production instantiation's own queue length (contribution counting on): what its exact stage ran
+    if (!COUNT && !BRE_SCAN_STATS && !BRE_PHASE_TIMING && count_c && lane == 0 && pf.queued != 0ull)
+        atomicAdd(&ctr->queued_pairs, pf.queued);
     if (BRE_SCAN_STATS && !COUNT && lane == 0) {
         atomicAdd(&ctr->candidates, ss_on);
         atomicAdd(&ctr->contributions, ss_kept);

@@ -347,22 +347,29 @@ BRE_TD ShapeSample sample_tri(const PTri &T, float u0, float u1) {
     return r;
 }
 
-// Distribution1D::SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389) over the
-// light powers; returns the light index (into light_tri)
-BRE_TD int sample_light(const DevScene &S, float u, float &pdf) {
-    const int size = S.n_lights + 1;
+// FindInterval, pbrt.h:377-389: bisection for the last index with pred true, then
+// Clamp(first - 1, 0, size - 2) (pbrt.h:278-284: the low bound is tested first)
+template <typename Pred>
+BRE_TD int find_interval(int size, const Pred &pred) {
     int first = 0, len = size;
     while (len > 0) {
         const int half = len >> 1, middle = first + half;
-        if (S.light_cdf[middle] <= u) {
+        if (pred(middle)) {
             first = middle + 1;
             len -= half + 1;
         } else {
             len = half;
         }
     }
-    int off = first - 1;
-    off = off < 0 ? 0 : (off > size - 2 ? size - 2 : off);
+    const int v = first - 1;
+    return v < 0 ? 0 : (v > size - 2 ? size - 2 : v);
+}
+
+// Distribution1D::SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389) over the
+// light powers; returns the light index (into light_tri)
+BRE_TD int sample_light(const DevScene &S, float u, float &pdf) {
+    const float *cdf = S.light_cdf;
+    const int off = find_interval(S.n_lights + 1, [&](int i) { return cdf[i] <= u; });
     pdf = (S.light_func_int > 0) ? S.light_func[off] / (S.light_func_int * (float)S.n_lights) : 0.f;
     return off;
 }

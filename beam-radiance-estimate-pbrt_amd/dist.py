@@ -56,7 +56,7 @@ class ShardedFrame:
         self.accum = torch.zeros((w * h, 3), dtype=torch.float32, device=device)
         self.device = device
         self._band = None
-        if world > 1 and not packets:
+        if not packets:  # the band machinery (also at world 1: a live 1-rank group still runs the gather)
             counts = [tile_pixels(w, h, r, world, tile, block).shape[0] for r in range(world)]
             self.band_len = max(counts)
             self._idx = torch.from_numpy(self.pixels).to(device)
@@ -82,14 +82,27 @@ class ShardedFrame:
                 self.accum.index_copy_(0, idx, parts[r][: idx.shape[0]].to(self.accum.device))
         return self.accum
 
-    def gather_to_root(self, root: int = 0):
-        """One collective per written image: each rank's band of owned pixels (packed, 1/N of the
-        film) is gathered to `root`, which scatters the bands into the full film.  Returns the full
-        film on the root (the rank's own partial film elsewhere)."""
+    def gather_bands(self, root: int = 0):
+        """Tile shards: the ranks' owned-pixel bands gathered to `root` (one collective); the list of
+        bands on the root, None elsewhere."""
         import torch
         import torch.distributed as dist
 
-        if self.world == 1:
+        band = self.band()
+        parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(band, gather_list=parts, dst=root)
+        return parts
+
+    def gather_to_root(self, root: int = 0):
+        """One collective per written image: each rank's band of owned pixels (packed, 1/N of the
+        film) is gathered to `root`, which scatters the bands into the full film.  Returns the full
+        film on the root (the rank's own partial film elsewhere).  Without a live process group a
+        one-rank frame is returned as it is; with one (also of size 1: tests/test_rccl_gpu.py) the
+        collective always runs."""
+        import torch.distributed as dist
+
+        live = dist.is_available() and dist.is_initialized()
+        if self.world == 1 and not live:
             return self.accum
         if self.packets:  # partial films of one image: one sum-reduce to the root
             if dist.get_backend() == "gloo" and self.accum.is_cuda:  # gloo reduces host tensors
@@ -100,9 +113,7 @@ class ShardedFrame:
             else:
                 dist.reduce(self.accum, dst=root, op=dist.ReduceOp.SUM)
             return self.accum
-        band = self.band()
-        parts = [torch.empty_like(band) for _ in range(self.world)] if self.rank == root else None
-        dist.gather(band, gather_list=parts, dst=root)
+        parts = self.gather_bands(root)
         if self.rank == root:
             self.scatter_bands(parts, skip=root)
         return self.accum

@@ -125,8 +125,10 @@ typedef struct bre_stats {
     int64_t n_camera_segments; /* segments of the last bre_camera_pass */
     double camera_ms;        /* device time of the last camera pass incl. compaction (timing only) */
     int64_t n_chunks;        /* kernel 5: chunks in the index of the last gather */
-    int64_t queued_pairs;    /* kernels 0/4, counters: (segment, beam) pairs that passed the prefilters
-                                and ran the exact stage (box test + ComputeClosestPoints) */
+    int64_t queued_pairs;    /* kernels 0/4: (segment, beam) pairs that passed the prefilters and ran the
+                                exact stage (box test + ComputeClosestPoints); counted with counters,
+                                and by the production instantiation itself whenever per-segment
+                                counts are requested (read back with counters or timing on) */
 } bre_stats;
 
 /* ---- context ---- */
@@ -272,6 +274,20 @@ float bre_beam_radius_at(float initial_radius, float alpha, int iteration);
 int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int32_t chunk);
 /* image = Ld / (iter + 1) for npix pixels (host arrays). */
 bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, float *out_rgb);
+
+/* ---- device self-check (tests) ----
+   Runs libbre's own device copies of the scalar primitives the passes and the gather share on n host
+   inputs x (synchronous; y is host memory):
+     kind 0: NextFloatUp(x)   1: NextFloatDown(x)   (pbrt.h:215-239; OffsetRayOrigin, geometry.h:1438-1458)
+     kind 2: y[2i] = the exact stage's square root (bre_math.h sqrt_cr_noscale), y[2i+1] = sqrtf(x)
+     kind 3: FindInterval(n_aux, [&](int k) { return aux[k] <= x; }) as a float (pbrt.h:377-389; the
+             light choice of Distribution1D::SampleDiscrete, sampling.h:90-100)
+     kind 4: y[2i] = x / aux[0] by the exact stage's shared-reciprocal division (div_by_shared),
+             y[2i+1] = x / aux[0] correctly rounded
+   so the tests can hold them against the reference's own primitive tests (src/tests/fp_tests.cpp,
+   find_interval.cpp) and against the compiler's correctly rounded sqrt and division. */
+bre_status bre_device_check(bre_ctx *ctx, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
+                            float *y);
 
 #ifdef __cplusplus
 }

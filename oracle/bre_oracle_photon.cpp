@@ -200,6 +200,32 @@ void ora_pcg32(uint64_t seq, int64_t n, int32_t as_float, uint32_t *out) {
     }
 }
 
+// PCG32 as pbrt's default-constructed RNG() (rng.h:129: PCG32_DEFAULT_STATE / _STREAM): n outputs of
+// UniformUInt32 (the stream fp_tests.cpp's NextUpDownFloat test draws its floats from)
+void ora_pcg32_default(int64_t n, uint32_t *out) {
+    orp::RNG r;
+    for (int64_t i = 0; i < n; ++i) out[i] = r.UniformUInt32();
+}
+
+// NextFloatUp (up != 0) / NextFloatDown of n floats (pbrt.h:215-239, the OffsetRayOrigin steps)
+void ora_next_float(int32_t up, int64_t n, const float *x, float *y) {
+    for (int64_t i = 0; i < n; ++i) y[i] = up ? orp::NextFloatUp(x[i]) : orp::NextFloatDown(x[i]);
+}
+
+// FloatToBits(BitsToFloat(u)) of n words (pbrt.h:191-202): the bit casts the float stepping uses
+void ora_float_bits(int64_t n, const uint32_t *u, uint32_t *out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = bre_f2u(bre_u2f(u[i]));
+}
+
+// FindInterval(n, [&](int i) { return a[i] <= x; }) for m values of x (pbrt.h:377-389), the search of
+// both Distribution1D samplers
+void ora_find_interval(const float *a, int32_t n, int64_t m, const float *x, int32_t *out) {
+    for (int64_t i = 0; i < m; ++i) {
+        const float v = x[i];
+        out[i] = orp::FindInterval(n, [&](int k) { return a[k] <= v; });
+    }
+}
+
 // PCG32 seeded like pcg32_srandom(initstate, initseq) (pbrt fixes initstate): for the
 // published test vector of the PCG reference implementation.
 void ora_pcg32_srandom(uint64_t initstate, uint64_t initseq, int64_t n, uint32_t *out) {

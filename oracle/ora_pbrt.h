@@ -248,6 +248,29 @@ struct Tri {
     bool emit;
 };
 
+// Clamp, pbrt.h:278-284 (low first: Clamp(x, 0, -1) of a one-entry array is 0 for x < 0, else -1)
+static inline int ClampInt(int val, int low, int high) {
+    if (val < low) return low;
+    if (val > high) return high;
+    return val;
+}
+// FindInterval, pbrt.h:377-389: the largest index i in [0, size - 2] with pred(i) true (pred is
+// monotone: true then false), by bisection; clamped to the first / last interval outside the range.
+template <typename Predicate>
+static inline int FindInterval(int size, const Predicate &pred) {
+    int first = 0, len = size;
+    while (len > 0) {
+        int half = len >> 1, middle = first + half;
+        if (pred(middle)) {
+            first = middle + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    return ClampInt(first - 1, 0, size - 2);
+}
+
 // Distribution1D, sampling.h:55-100: the piecewise-constant CDF of func (the constructor) and
 // SampleDiscrete with FindInterval (sampling.h:90-100, pbrt.h:377-389)
 struct Distribution1D {
@@ -266,18 +289,7 @@ struct Distribution1D {
     }
     int Count() const { return (int)func.size(); }
     int SampleDiscrete(Float u, Float *pdf, Float *uRemapped = nullptr) const {
-        const int size = (int)cdf.size();
-        int first = 0, len = size;
-        while (len > 0) {
-            int half = len >> 1, middle = first + half;
-            if (cdf[middle] <= u) {
-                first = middle + 1;
-                len -= half + 1;
-            } else {
-                len = half;
-            }
-        }
-        const int offset = std::min(std::max(first - 1, 0), size - 2);  // Clamp(first - 1, 0, size - 2)
+        const int offset = FindInterval((int)cdf.size(), [&](int i) { return cdf[i] <= u; });
         if (pdf) *pdf = (funcInt > 0) ? func[offset] / (funcInt * (Float)Count()) : 0;
         if (uRemapped) *uRemapped = (u - cdf[offset]) / (cdf[offset + 1] - cdf[offset]);
         return offset;
@@ -285,18 +297,7 @@ struct Distribution1D {
     Float DiscretePDF(int index) const { return func[index] / (funcInt * (Float)Count()); }
     // SampleContinuous (sampling.h:71-89): the same FindInterval, then the offset along the segment
     Float SampleContinuous(Float u, Float *pdf, int *off = nullptr) const {
-        const int size = (int)cdf.size();
-        int first = 0, len = size;
-        while (len > 0) {
-            int half = len >> 1, middle = first + half;
-            if (cdf[middle] <= u) {
-                first = middle + 1;
-                len -= half + 1;
-            } else {
-                len = half;
-            }
-        }
-        const int offset = std::min(std::max(first - 1, 0), size - 2);
+        const int offset = FindInterval((int)cdf.size(), [&](int i) { return cdf[i] <= u; });
         if (off) *off = offset;
         Float du = u - cdf[offset];
         if ((cdf[offset + 1] - cdf[offset]) > 0) du /= (cdf[offset + 1] - cdf[offset]);

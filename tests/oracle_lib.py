@@ -65,6 +65,10 @@ class Oracle:
         lib.ora_tri_sample.argtypes = [P, I32, I64, P, P, P, P]
         lib.ora_distribution1d.argtypes = [P, I32, I64, P, P, P, P, P]
         lib.ora_distribution1d_continuous.argtypes = [P, I32, I64, P, P, P, P]
+        lib.ora_pcg32_default.argtypes = [I64, P]
+        lib.ora_next_float.argtypes = [I32, I64, P, P]
+        lib.ora_float_bits.argtypes = [I64, P, P]
+        lib.ora_find_interval.argtypes = [P, I32, I64, P, P]
         lib.ora_tri_reintersect.argtypes = [I32, I32, P, P]
         lib.ora_scene_intersect.argtypes = [P, I64, P, P, I32, P, P, P]
         lib.ora_tri_reintersect.restype = I64
@@ -198,6 +202,30 @@ class Oracle:
         x, pdf, off = np.zeros(m, np.float32), np.zeros(m, np.float32), np.zeros(m, np.int32)
         self.lib.ora_distribution1d_continuous(_p(func), func.shape[0], m, _p(u), _p(x), _p(pdf), _p(off))
         return x, pdf, off
+
+    def pcg32_default(self, n):  # RNG() (rng.h:129)
+        out = np.zeros(n, np.uint32)
+        self.lib.ora_pcg32_default(n, _p(out))
+        return out
+
+    def next_float(self, x, up=True):  # NextFloatUp / NextFloatDown (pbrt.h:215-239)
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        y = np.zeros_like(x)
+        self.lib.ora_next_float(int(up), x.shape[0], _p(x), _p(y))
+        return y
+
+    def float_bits(self, u):  # FloatToBits(BitsToFloat(u)) (pbrt.h:191-202)
+        u = np.ascontiguousarray(u, dtype=np.uint32)
+        out = np.zeros_like(u)
+        self.lib.ora_float_bits(u.shape[0], _p(u), _p(out))
+        return out
+
+    def find_interval(self, a, x):  # FindInterval(n, a[i] <= x) (pbrt.h:377-389)
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        out = np.zeros(x.shape[0], np.int32)
+        self.lib.ora_find_interval(_p(a), a.shape[0], x.shape[0], _p(x), _p(out))
+        return out
 
     def tri_reintersect(self, n_tris=1000, rays_per_tri=10000):
         """Triangle.Reintersect (shapes.cpp:154-208): (re-intersections, rays tested, triangles used)."""

@@ -412,6 +412,44 @@ def test_transposed_scan_is_bit_identical(bre, synth, kind):
         assert np.array_equal(outs[t]["counts"][:, 1], outs[0]["counts"][:, 1]), t
 
 
+def test_transposed_scan_skips_packet_rejected_parallel_beams(bre, oracle):
+    """a beam the packet rejects is staged with thr_sq = -inf, but scan_keep_mask only
+    rejects when u >= 0.0101, so a rejected beam nearly parallel to the segments would get a keep bit
+    in the transposed scan (lane = beam) unless the push is masked with the packet's kept beams.  One
+    leaf tile holds 24 beams crossing a packet of 64 parallel segments and 40 beams parallel to them
+    but far away (packet box reject).  The production kernel's own queue length (counted whenever
+    per-segment counts are asked for) must be the same with the transposed scan forced on (threshold
+    64) and off (0), and so must every output bit."""
+    rng = np.random.default_rng(5)
+    n_seg = 64
+    o = np.stack([np.full(n_seg, 0.1), np.linspace(0.10, 0.20, n_seg), np.full(n_seg, 0.5)], 1).astype(np.float32)
+    d = np.tile(np.array([1.0, 0.0, 0.0], np.float32), (n_seg, 1))
+    segs = {"o": o, "p": (o + d * np.float32(0.8)).astype(np.float32), "d": d,
+            "tmax": np.full(n_seg, 0.8, np.float32)}
+    xs = rng.uniform(0.15, 0.85, 24).astype(np.float32)
+    cross_s = np.stack([xs, np.full(24, 0.15), np.full(24, 0.2)], 1).astype(np.float32)
+    cross_e = np.stack([xs, np.full(24, 0.15), np.full(24, 0.8)], 1).astype(np.float32)
+    y = rng.uniform(0.80, 0.90, 40).astype(np.float32)
+    par_s = np.stack([np.full(40, 0.1), y, np.full(40, 0.5)], 1).astype(np.float32)
+    par_e = np.stack([np.full(40, 0.9), y + np.float32(1e-3), np.full(40, 0.5)], 1).astype(np.float32)
+    beams = {"start": np.concatenate([cross_s, par_s]), "end": np.concatenate([cross_e, par_e]),
+             "radius": np.full(64, 0.01, np.float32), "power": rng.random((64, 3), np.float32)}
+    R = 0.02
+    ref = oracle.build(beams).gather(segs, R)
+    assert ref["contrib"].sum() > 0
+    outs, queued = {}, {}
+    for t in (0, 64):
+        with bre.BeamGather(0, counters=False, timing=True, kernel=0) as g:
+            g.set_option(108, t)
+            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
+            outs[t] = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], R=R, counts=True)
+            queued[t] = g.stats()["queued_pairs"]
+    assert np.array_equal(outs[64]["counts"][:, 1], ref["contrib"])
+    assert queued[0] > 0
+    assert queued[64] == queued[0], queued
+    assert np.array_equal(outs[64]["seg_rgb"], outs[0]["seg_rgb"])
+
+
 def test_removed_kernels_are_rejected(bre):
     with bre.BeamGather(0) as g:
         for k in (1, 3, 6, 7):

@@ -176,3 +176,40 @@ def test_distribution1d_continuous(oracle):  # sampling.cpp:282-303
     assert x[2] == pytest.approx(0.9, rel=4 * 2.0 ** -23)  # middle of the 8 segment
     assert pdf[2] == pytest.approx(5 * 8.0 / 16.0, rel=4 * 2.0 ** -23) and off[2] == 4
     assert x[3] == pytest.approx(1.0, rel=4 * 2.0 ** -23)
+
+
+def test_find_interval_basics(oracle):  # find_interval.cpp:8-28 (FindInterval.Basics)
+    a = np.arange(10, dtype=np.float32)
+    assert oracle.find_interval(a, np.array([-1.0], np.float32))[0] == 0  # clamped below
+    assert oracle.find_interval(a, np.array([100.0], np.float32))[0] == a.size - 2  # clamped above
+    for i in range(a.size - 1):
+        assert oracle.find_interval(a, np.array([i], np.float32))[0] == i
+        assert oracle.find_interval(a, np.array([i + 0.5], np.float32))[0] == i
+        if i > 0:
+            assert oracle.find_interval(a, np.array([i - 0.5], np.float32))[0] == i - 1
+
+
+def _pbrt_floats(oracle, n):  # GetFloat (fp_tests.cpp:12-18): RNG() words as floats, NaNs skipped
+    u = oracle.pcg32_default(2 * n)
+    f = u.view(np.float32)
+    return f[~np.isnan(f)][:n]
+
+
+def test_next_up_down_float(oracle):  # fp_tests.cpp:29-53 (FloatingPoint.NextUpDownFloat)
+    inf = np.float32(np.inf)
+    up = oracle.next_float(np.array([-0.0, inf, -inf], np.float32), up=True)
+    dn = oracle.next_float(np.array([0.0, inf, -inf], np.float32), up=False)
+    assert up[0] > 0.0 and dn[0] < 0.0
+    assert up[1] == inf and dn[1] < inf
+    assert dn[2] == -inf and up[2] > -inf
+    f = _pbrt_floats(oracle, 100_000)
+    f = f[np.isfinite(f)]
+    assert f.size > 99_000
+    assert np.array_equal(oracle.next_float(f, True).view(np.uint32), np.nextafter(f, inf).view(np.uint32))
+    assert np.array_equal(oracle.next_float(f, False).view(np.uint32), np.nextafter(f, -inf).view(np.uint32))
+
+
+def test_float_bits(oracle):  # fp_tests.cpp:70-79 (FloatingPoint.FloatBits), RNG(1)
+    u = oracle.pcg32(1, 100_000)
+    keep = ~np.isnan(u.view(np.float32))
+    assert np.array_equal(oracle.float_bits(u[keep]), u[keep])
