@@ -66,7 +66,7 @@ struct bre_ctx {
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
     int tile_axis = 0;       // internal: tile kernel tile axis reject (GatherArgs::tileax), 1 = on (measured slower)
-    int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
+    int occupancy = 5;       // tile kernel register budget (min waves per SIMD): 5 = the LDS bound of the round-4 tile planes (7.5 KB per wave)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
@@ -86,6 +86,7 @@ struct bre_ctx {
     bool sort_segments = true;
     DevMem ss_bounds, ss_keys, ss_keys_alt, ss_vals, ss_vals_alt, ss_tmp, ss_o, ss_p, ss_d, ss_t, ss_pix;
     DevMem sp_o, sp_p, sp_d, sp_t, sp_pix, sp_index;  // this packet shard's segments (contiguous)
+    DevMem px_seg, px_keys, px_keys_alt, px_vals, px_vals_alt, px_tmp;  // deterministic per-pixel compose
     // beam set
     int64_t nbeams = 0, nvalid = 0, nnodes = 0;
     BeamSet bset;  // the built set's radius layout (BeamRec)
@@ -588,7 +589,9 @@ void bre_destroy(bre_ctx *c) {
                      &c->ch_par, &c->ch_recs, &c->ch_cpar, &c->ch_nodes, &c->ss_bounds, &c->ss_keys,
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
                      &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index,
-                     &c->gbox, &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf};
+                     &c->gbox, &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf,
+                     &c->px_seg, &c->px_keys, &c->px_keys_alt, &c->px_vals, &c->px_vals_alt, &c->px_tmp,
+                     &c->chk_x, &c->chk_aux, &c->chk_y};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
@@ -1056,9 +1059,9 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
 // (bre_shard_segments): the other entries of the per-segment outputs are zeroed, and the shards'
 // films and outputs sum to the one-shard results.  Used by bre_gather_camera (the camera pass's
 // segments), bre_gather_device and bre_gather (the caller's segments).
-static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const float *p, const float *d,
-                                  const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
-                                  float *d_seg_rgb, int32_t *d_seg_counts) {
+static bre_status gather_segments_core(bre_ctx *c, int64_t n, const float *o, const float *p, const float *d,
+                                       const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
+                                       float *d_seg_rgb, int32_t *d_seg_counts) {
     const bool pshard = c->shard_mode == 1 && c->shard_count > 1;
     const bool sortable = c->kernel == 0 || c->kernel == 4;  // kernels 2 / 5 write in the caller's order
     const bool seg_out = d_seg_rgb || d_seg_counts;
@@ -1122,6 +1125,41 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
     if (pshard) return pick(ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, c->ss_vals_alt.as<int32_t>());
     return gather_device(c, n, ss.o2, ss.p2, ss.d2, ss.t2, pix ? ss.pix2 : nullptr, R, npix, d_accum, d_seg_rgb,
                          d_seg_counts, seg_out ? c->ss_vals_alt.as<int32_t>() : nullptr);
+}
+
+// A gather of n caller-order segments.  With a film (d_accum) the production kernels (0 / 4) add to it
+// deterministically: the per-segment sums go to a buffer in the caller's order (the caller's d_seg_rgb
+// or an internal one; under packet shards the other shards' entries are 0), then launch_pixel_compose
+// adds each pixel's segments in the caller's order -- for the camera pass, the path depths in order,
+// as the reference's pixel.Ld += does (photonbeam.cpp:477-504) -- with one thread per pixel and no
+// float atomics, so the film is the same bits on every run.  Kernels 2 and 5 (cross-checks) add by
+// float atomics.
+static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const float *p, const float *d,
+                                  const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
+                                  float *d_seg_rgb, int32_t *d_seg_counts) {
+    const bool sortable = c->kernel == 0 || c->kernel == 4;
+    if (!d_accum || !sortable || n <= 0 || !pix || c->nvalid == 0)
+        return gather_segments_core(c, n, o, p, d, t, pix, R, npix, d_accum, d_seg_rgb, d_seg_counts);
+    const size_t N = (size_t)n;
+    float *segbuf = d_seg_rgb;
+    if (!segbuf) {
+        HIPCHK(c, c->px_seg.ensure(N * 3 * sizeof(float)));
+        segbuf = c->px_seg.as<float>();
+    }
+    bre_status st = gather_segments_core(c, n, o, p, d, t, pix, R, npix, nullptr, segbuf, d_seg_counts);
+    if (st != BRE_OK) return st;
+    HIPCHK(c, c->px_keys.ensure(N * sizeof(unsigned int)));
+    HIPCHK(c, c->px_keys_alt.ensure(N * sizeof(unsigned int)));
+    HIPCHK(c, c->px_vals.ensure(N * sizeof(int32_t)));
+    HIPCHK(c, c->px_vals_alt.ensure(N * sizeof(int32_t)));
+    const size_t tb = pixel_sort_temp_bytes(n);
+    HIPCHK(c, c->px_tmp.ensure(tb + 16));
+    DevCounters *ctr = c->counters_buf.as<DevCounters>();  // allocated by the gather above
+    PixelCompose pc{n, pix, segbuf, npix, d_accum, c->px_keys.as<unsigned int>(), c->px_keys_alt.as<unsigned int>(),
+                    c->px_vals.as<int32_t>(), c->px_vals_alt.as<int32_t>(), c->px_tmp.ptr, tb, &ctr->flags,
+                    kFlagPixel};
+    HIPCHK(c, launch_pixel_compose(pc, c->stream));
+    return BRE_OK;
 }
 
 // The camera segments of the last camera pass against the beam set (gather_segments).

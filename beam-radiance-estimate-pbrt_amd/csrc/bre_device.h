@@ -243,6 +243,24 @@ struct SegSort {
                    // 4: Hilbert order of (origin, end point) (the default, bre_math.h hilbert_key)
 };
 size_t seg_sort_temp_bytes(int64_t n);
+// deterministic per-pixel accumulation of per-segment sums (bre_sort.hip): stable sort of the
+// segments by pixel, then one thread per pixel adds its segments in the caller's order
+struct PixelCompose {
+    int64_t n;
+    const int32_t *pix;      // [n] pixel of each segment
+    const float *seg_rgb;    // [3n] per-segment sums
+    int64_t npix;
+    float *accum;            // [3 npix] += per pixel
+    unsigned int *keys, *keys_alt;
+    int32_t *vals, *vals_alt;
+    void *tmp;
+    size_t tmp_bytes;
+    unsigned int *flags;     // DevCounters::flags
+    unsigned int bad_pixel_flag;
+};
+size_t pixel_sort_temp_bytes(int64_t n);
+hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st);
+
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);
 hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,
                               const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,

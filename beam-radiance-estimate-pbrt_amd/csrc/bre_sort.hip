@@ -288,6 +288,49 @@ __global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, in
     (void)n;
 }
 
+// Deterministic per-pixel accumulation of a gather's per-segment sums (PixelCompose).  The reference
+// adds a pixel's gather terms in one fixed order (one thread per 16x16 tile, the pixel's path depths
+// in order, photonbeam.cpp:477-504); float atomics would add a pixel's segments in arrival order and
+// let the film differ in the last bits from run to run.  Instead the segments are stably sorted by
+// pixel (so a pixel's segments keep the caller's order: the camera pass's depth order), and one
+// thread per pixel adds its run of segment sums in that order and then adds the run's sum to the film.
+__global__ __launch_bounds__(kBlock) void k_pix_keys(int64_t n, const int32_t *__restrict__ pix, int64_t npix,
+                                                     unsigned int *__restrict__ keys, int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int32_t p = pix[i];
+    keys[i] = (p < 0 || (int64_t)p >= npix) ? (unsigned int)npix : (unsigned int)p;  // npix: invalid
+    vals[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pix_compose(int64_t n, const unsigned int *__restrict__ keys,
+                                                        const int32_t *__restrict__ vals,
+                                                        const float *__restrict__ seg_rgb, int64_t npix,
+                                                        float *__restrict__ accum, unsigned int *__restrict__ flags,
+                                                        unsigned int bad_pixel_flag) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const unsigned int k = keys[i];
+    if (i > 0 && keys[i - 1] == k) return;  // not the first segment of its pixel
+    if ((int64_t)k >= npix) {
+        atomicOr(flags, bad_pixel_flag);  // a seg_pixel outside [0, npix): never silent (check_flags)
+        return;
+    }
+    float r = 0.f, g = 0.f, b = 0.f;
+    for (int64_t j = i; j < n && keys[j] == k; ++j) {
+        const int64_t s = vals[j];
+        r += seg_rgb[3 * s];
+        g += seg_rgb[3 * s + 1];
+        b += seg_rgb[3 * s + 2];
+    }
+    if (r != 0.f || g != 0.f || b != 0.f) {
+        float *a = accum + 3 * (int64_t)k;
+        a[0] += r;
+        a[1] += g;
+        a[2] += b;
+    }
+}
+
 }  // namespace
 
 hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,
@@ -333,6 +376,28 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
                        s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);
+    return hipGetLastError();
+}
+
+size_t pixel_sort_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned int *)nullptr, (unsigned int *)nullptr,
+                                    (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 32);
+    return bytes;
+}
+
+hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st) {
+    if (c.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pix_keys, dim3(grid_of(c.n)), dim3(kBlock), 0, st, c.n, c.pix, c.npix, c.keys, c.vals);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    int bits = 1;
+    while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)c.npix) ++bits;  // keys in [0, npix]
+    size_t bytes = c.tmp_bytes;
+    e = rocprim::radix_sort_pairs(c.tmp, bytes, c.keys, c.keys_alt, c.vals, c.vals_alt, (size_t)c.n, 0, bits, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pix_compose, dim3(grid_of(c.n)), dim3(kBlock), 0, st, c.n, c.keys_alt, c.vals_alt, c.seg_rgb,
+                       c.npix, c.accum, c.flags, c.bad_pixel_flag);
     return hipGetLastError();
 }
 

@@ -30,10 +30,10 @@ Also reported (rank 0, N = 1):
   path's TA / TD busy fractions with the busiest unit named -- since round 3 the TD data-return
   path); `traffic` = HBM bytes per
   launch from the same passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE).  `hbm`: the
-  algorithmic bytes per launch (node and beam lines of the visited tiles, the segments, the exact
-  stage's 112 B per queued pair, the partial sums; counted live by the counter pass) / the launch's
+  requested bytes per launch (node and beam lines of the visited tiles, the segments, the exact
+  stage's 48 B of SegRec per queued pair, the partial sums; counted live by the counter pass) / the launch's
   HIP-event time against 8 TB/s, and the measured HBM traffic against it.  Without rocprofv3 the
-  line falls back to `bound` "hbm" on the algorithmic bytes.  The SURVEY §8d reference-tree byte
+  line falls back to `bound` "hbm" on the requested bytes.  The SURVEY §8d reference-tree byte
   model is kept as `ref_model_*` (not a fraction: one staged beam line feeds 64 lanes).
 * `cpu_baseline` — the oracle's CPU restatement of the reference algorithm (SAH tree, per-query
   vector<shared_ptr>, all host threads, plus 1 thread), timed on bounded samples of the same
@@ -202,35 +202,7 @@ def main():
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
                               packets=args.shard_mode == "packets")
     def make_ctx():
-        c = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
-                           prefilter=bool(args.prefilter))
-        c.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
-        if args.kernel == 5:
-            c.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
-            c.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
-        if args.occupancy:
-            c.set_option(102, args.occupancy)
-        if args.tile_leaf:
-            c.set_option(bre.OPT_TILE_LEAF, args.tile_leaf)
-        if args.block_map >= 0:
-            c.set_option(107, args.block_map)
-        if args.sort_key >= 0:
-            c.set_option(105, args.sort_key)
-        if args.tscan >= 0:
-            c.set_option(108, args.tscan)
-        if args.beam_key >= 0:
-            c.set_option(110, args.beam_key)
-        if args.margin >= 0:
-            c.set_option(111, args.margin)
-        if args.tile_axis >= 0:
-            c.set_option(112, args.tile_axis)
-        if args.split_records >= 0:
-            c.set_option(113, args.split_records)
-        # one explicit stream per context, shared with torch: the HIP events that time the gather
-        # kernel are recorded on the stream the kernel runs on
-        st = torch.cuda.Stream(dev)
-        c.set_stream(st.cuda_stream)
-        return c, st
+        return make_context(bre, args, dev)
 
     g, stream = make_ctx()
     torch.cuda.set_stream(stream)
@@ -288,13 +260,21 @@ def main():
         total_seg = nseg_local
     value = total_seg / elapsed
 
-    # untimed: one more step with counters and per-phase HIP-event timing inside libbre
-    diag, st = {}, None
+    # untimed: one more step with counters and per-phase HIP-event timing inside libbre, at iteration 0
+    # (the largest radius: the roofline's launch) and at the last timed step's iteration (the smallest
+    # radius the line times: the scan-bound end of the render)
+    diag, st, st_last = {}, None, None
     if not args.no_diag:
         g.set_option(bre.OPT_COUNTERS, 1)
         g.set_option(bre.OPT_TIMING, 1)
-        diag = wl.diagnostics()
+        diag = wl.diagnostics(0)
         st = g.stats()
+        k_last = args.steps - 1
+        if getattr(wl, "iteration", None) and wl.iteration(k_last) != wl.iteration(0):
+            d_last = wl.diagnostics(k_last)
+            st_last = g.stats()
+            st_last["_iteration"] = wl.iteration(k_last)
+            st_last["_gather_ms"] = d_last.get("gather_ms_iter0")
         g.set_option(bre.OPT_COUNTERS, 0)
         g.set_option(bre.OPT_TIMING, 0)
 
@@ -318,22 +298,14 @@ def main():
         "gather_ms_per_step": gather_per_step if rank == 0 else None,
     }
     if st is not None:
-        nseg_d = max(st["n_segments"], 1)
-        items = (nseg_d + 63) // 64 * args.split  # (packet, subtree) work items = waves
-        result.update({
-            "candidates_per_estimate": st["candidates"] / nseg_d,
-            "contributions_per_estimate": st["contributions"] / nseg_d,
-            "candidate_pair_tests_per_s": st["candidates"] / nseg_d * value,
-            "node_visits_per_wave": st["node_visits"] / items,
-            "leaf_visits_per_wave": st["leaf_visits"] / items,
-            "beam_lines_staged_per_wave": st["beam_evals"] / items,
-            "exact_batches_per_wave": st["ccp_wave_evals"] / items,
-            "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
-            "queued_pairs_per_estimate": st["queued_pairs"] / nseg_d,
-            "contributions_per_queued_pair": st["contributions"] / max(st["queued_pairs"], 1),
-            # (lane, kept beam) prefilter tests ~ kept beams x 64 lanes; per queued pair (~7)
-            "prefilter_tests_per_queued_pair": st["useful_beam_evals"] * 64 / max(st["queued_pairs"], 1),
-        })
+        result.update(counter_block(st, args))
+        result["candidate_pair_tests_per_s"] = result["candidates_per_estimate"] * value
+    if st_last is not None:
+        # the same counter block at the last timed iteration (the late, small-radius
+        # iterations are scan-bound and their funnel belongs in the line)
+        last = counter_block(st_last, args)
+        last.update({"iteration": st_last["_iteration"], "gather_ms": st_last["_gather_ms"]})
+        result["counters_last_iteration"] = last
     result.update(diag)
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -359,6 +331,46 @@ def main():
         dist.destroy_process_group()
 
 
+def make_context(bre, args, dev):
+    """One libbre context with the bench's options, on its own torch stream (the HIP events that time
+    the gather are recorded on the stream the kernel runs on).  Returns (context, stream)."""
+    import torch
+
+    c = bre.BeamGather(dev.index, kernel=args.kernel, leaf_size=args.leaf_size, split=args.split,
+                       prefilter=bool(args.prefilter))
+    c.set_option(bre.OPT_SORT_SEGMENTS, args.sort_segments)
+    if args.kernel == 5:
+        c.set_option(bre.OPT_CHUNK_LEN, args.chunk_len)
+        c.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
+    for opt, val in ((102, args.occupancy if args.occupancy else -1), (bre.OPT_TILE_LEAF, args.tile_leaf or -1),
+                     (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
+                     (111, args.margin), (112, args.tile_axis), (113, args.split_records)):
+        if val >= 0:
+            c.set_option(opt, val)
+    st = torch.cuda.Stream(dev)
+    c.set_stream(st.cuda_stream)
+    return c, st
+
+
+def counter_block(st, args):
+    """libbre's counters of one gather (counting instantiation) as per-estimate / per-wave figures."""
+    nseg_d = max(st["n_segments"], 1)
+    items = (nseg_d + 63) // 64 * args.split  # (packet, subtree) work items = waves
+    return {
+        "candidates_per_estimate": st["candidates"] / nseg_d,
+        "contributions_per_estimate": st["contributions"] / nseg_d,
+        "node_visits_per_wave": st["node_visits"] / items,
+        "leaf_visits_per_wave": st["leaf_visits"] / items,
+        "beam_lines_staged_per_wave": st["beam_evals"] / items,
+        "exact_batches_per_wave": st["ccp_wave_evals"] / items,
+        "bundle_keep_frac": st["useful_beam_evals"] / max(st["beam_evals"], 1),
+        "queued_pairs_per_estimate": st["queued_pairs"] / nseg_d,
+        "contributions_per_queued_pair": st["contributions"] / max(st["queued_pairs"], 1),
+        # (lane, kept beam) prefilter tests ~ kept beams x 64 lanes; per queued pair (VERDICT r2: ~7)
+        "prefilter_tests_per_queued_pair": st["useful_beam_evals"] * 64 / max(st["queued_pairs"], 1),
+    }
+
+
 def roofline(st, args, wl, gather_ms, pmc, cpu):
     """Roofline of the tile kernel for one launch of iteration 0 (see the module docstring).
 
@@ -366,28 +378,30 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     fractions of the vector-memory path, the busiest unit since round 3): `achieved` = the launch's wave64 VALU instructions
     (SQ_INSTS_VALU) per second, `peak` = 256 CU x 4 SIMD x one wave64 instruction per 2 clocks at the
     clock the same counters measured, so `frac` = the VALU issue fraction.  The byte side is kept in
-    `hbm`: the algorithmic bytes the packets request per launch against the 8 TB/s HBM peak (served
+    `hbm`: the bytes the packets request per launch against the 8 TB/s HBM peak (served
     mostly from L1 / L2 / Infinity Cache: the requests exceed what HBM could deliver) and the HBM
     traffic the FETCH/WRITE counters measure.  Without the PMC passes the line falls back to the HBM
-    roofline of the algorithmic bytes."""
+    roofline of the requested bytes."""
     nseg = max(st["n_segments"], 1)
     items = (nseg + 63) // 64 * args.split
-    # what the packet algorithm must read / write per launch: every visited node line and staged
-    # beam line (64 B each) of every (packet, subtree) item; per item the segments (40 B in) and the
-    # per-subtree partial sums (12 B out) of its 64 lanes; per queued (lane, beam) pair the exact
-    # stage's loads (three of the segment's 16-B SegRec planes -- the unit direction is recomputed --
-    # and the 64-B BeamRec, which carries the power of the photon pass's uniform-radius beams: 112 B;
-    # 128 B with the split layout, option 113); and the reduce (12 B x split in, 12 B out per segment)
+    # what the packet algorithm requests from the memory hierarchy per launch (L1 / TA level): every
+    # visited node line and staged beam line (64 B each) of every (packet, subtree) item; per item the
+    # segments (40 B in) and the per-subtree partial sums (12 B out) of its 64 lanes; per queued
+    # (lane, beam) pair the exact stage's three 16-B SegRec planes (48 B: since round 4 the beam comes
+    # from the tile's LDS planes, and the unit direction is recomputed; + 16 B power of a mixed-radius
+    # set); and the reduce (12 B x split in, 12 B out per segment)
     queued = st.get("queued_pairs", 0)
-    pair_b = 128.0 if args.split_records == 1 else 112.0
-    alg = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + pair_b * queued
+    pair_b = 64.0 if args.split_records == 1 else 48.0
+    req = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + pair_b * queued
            + nseg * 12 * (args.split + 1))
-    requested = alg / (gather_ms * 1e-3) / 1e9
+    requested = req / (gather_ms * 1e-3) / 1e9
     hbm = {"requested_GBps": requested, "peak": HBM_PEAK_GBPS, "requested_over_peak": requested / HBM_PEAK_GBPS,
-           "algorithmic_bytes_per_launch": alg, "queued_pairs_per_launch": queued,
-           "algorithmic_model": "64 B x (node visits + beam lines staged) + 52 B x 64 per (packet, subtree) "
-                                f"item + {pair_b:.0f} B per queued exact-stage pair + 12 B x (split + 1) per segment; "
-                                "counts from this run's counter pass"}
+           "requested_bytes_per_launch": req, "queued_pairs_per_launch": queued,
+           "requested_model": "bytes the packets request at the L1 / texture-address level: 64 B x (node "
+                              "visits + beam lines staged) + 52 B x 64 per (packet, subtree) item + "
+                              f"{pair_b:.0f} B per queued exact-stage pair + 12 B x (split + 1) per segment; counts "
+                              "from this run's counter pass.  Served mostly by L1 / L2 / Infinity Cache: compare "
+                              "traffic_bytes_per_launch (HBM) and the l2 block"}
     out = {"bound": "hbm", "achieved": requested, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
            "frac": requested / HBM_PEAK_GBPS, "traffic": None,
            "kernel": "k_gather_tile (+ k_reduce)", "launch": "iteration 0", "launch_ms": gather_ms}
@@ -398,7 +412,9 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
             hbm["traffic_bytes_per_launch"] = out["traffic"]
             hbm["traffic_GBps"] = out["traffic"] / (pmc["kernel_ms"] * 1e-3) / 1e9
             hbm["traffic_frac"] = hbm["traffic_GBps"] / HBM_PEAK_GBPS
-            hbm["traffic_over_algorithmic"] = out["traffic"] / alg
+            hbm["traffic_over_requested"] = out["traffic"] / req
+        if pmc.get("l2"):
+            out["l2"] = pmc["l2"]
         iss = pmc.get("issue")
         if iss:
             t = pmc["kernel_ms"] * 1e-3
@@ -427,7 +443,10 @@ PMC_PASSES = {
            "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"],
     # the vector-memory path: address (TA) and data-return (TD) units, one each per CU
     "vmem": ["TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "SQ_INSTS_VMEM_RD"],
+    # where the requests are served: L2 hits / misses and the L1 -> L2 read requests (optional pass)
+    "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
 }
+PMC_OPTIONAL = {"l2"}
 
 
 def pmc_passes(args):
@@ -453,8 +472,12 @@ def pmc_passes(args):
         try:
             r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150)
         except subprocess.TimeoutExpired:
+            if name in PMC_OPTIONAL:
+                continue
             return None
         if r.returncode != 0:
+            if name in PMC_OPTIONAL:
+                continue
             return None
         cc = kt = None
         for root_, _, files in os.walk(d):
@@ -464,6 +487,8 @@ def pmc_passes(args):
                 if f.endswith("kernel_trace.csv"):
                     kt = os.path.join(root_, f)
         if not cc:
+            if name in PMC_OPTIONAL:
+                continue
             return None
         for row in csv.DictReader(open(cc)):
             if "k_gather_tile" in row["Kernel_Name"]:
@@ -504,6 +529,12 @@ def pmc_passes(args):
             units = {"valu_issue": iss["valu_issue_frac"], "lds": iss["lds_busy_frac"],
                      "vmem_address_ta": iss["ta_busy_frac"], "vmem_data_td": iss["td_busy_frac"]}
             iss["busiest_unit"] = max(units, key=units.get)
+    if "TCC_HIT_sum" in vals and "TCC_MISS_sum" in vals:
+        h, m = vals["TCC_HIT_sum"], vals["TCC_MISS_sum"]
+        res["l2"] = {"TCC_HIT_sum": h, "TCC_MISS_sum": m, "hit_rate": h / max(h + m, 1.0),
+                     "TCP_TCC_READ_REQ_sum": vals.get("TCP_TCC_READ_REQ_sum"),
+                     "note": "L2 (TCC) requests of the iteration-0 launch: hits are served on the XCD, misses go "
+                             "to the Infinity Cache / HBM (FETCH_SIZE); TCP_TCC_READ_REQ = L1 misses sent to L2"}
     return res
 
 
@@ -530,10 +561,14 @@ class SceneWorkload:
             c.set_shard(shard_rank, shard_count, frame.block, frame.packets)
         self.shard = (shard_rank, shard_count)
         self.ld = frame.accum
-        # one film per context: the camera pass adds surface radiance without atomics, so two
-        # iterations in flight must not share a buffer; finish() sums them
-        self.films = [self.ld] + [torch.zeros_like(self.ld) for _ in ctxs[1:]]
-        self.scratch = [torch.zeros_like(self.ld) for _ in ctxs]
+        # one iteration image per context (the camera pass's surface radiance, then the gather's
+        # per-pixel sums, both deterministic: libbre adds a pixel's segments in depth order without
+        # atomics), added to the ONE film in iteration order -- each add waits for the previous
+        # iteration's add, whatever stream it ran on -- so the film's bits do not depend on the
+        # number of contexts (tests/test_film_determinism_gpu.py)
+        self.iter_img = [torch.zeros_like(self.ld) for _ in ctxs]
+        self.scratch_film = torch.zeros_like(self.ld)
+        self._last_add = None  # event after the previous iteration's film add
         self.data = (f"synthetic scene (SURVEY.md §8d {self.name.upper()}: built-in Cornell box + "
                      f"{'grid-density smoke' if preset['medium'] == 'smoke' else 'homogeneous fog'}; photons and "
                      "camera paths traced on the GPU)")
@@ -577,17 +612,19 @@ class SceneWorkload:
         self._rec[it] = rec
         return rec
 
-    def step(self, k, ev, scratch):
+    def step(self, k, ev, scratch, ctx=None):
         import torch
 
         a = self.args
         it = self.iteration(k)
-        i = k % len(self.ctxs)
+        i = k % len(self.ctxs) if ctx is None else ctx
         g, st = self.ctxs[i]
-        ld = (self.scratch if scratch else self.films)[i]
+        ld = self.iter_img[i]
+        film = self.scratch_film if scratch else self.ld
         R = self.radius(it)
         rec = self.recorder_segments(it) if a.entry == "boundary" else None
         with torch.cuda.stream(st):
+            ld.zero_()
             self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
             if rec is None:
                 n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
@@ -601,31 +638,32 @@ class SceneWorkload:
                 g.gather_device(rec["o"], rec["p"], rec["d"], rec["tmax"], rec["pixel"], R, self.W * self.H, accum=ld)
             if ev is not None:
                 ev[1].record()
+            if self._last_add is not None:
+                st.wait_event(self._last_add)
+            film.add_(ld)
+            self._last_add = torch.cuda.Event()
+            self._last_add.record(st)
         if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
             n = self.bre.shard_segments(n, *self.shard, self.frame.block)
         self.last_nseg = n
         return n
 
     def finish(self):
-        """Sum the pipeline's films into the frame (on the first context's stream, after both)."""
+        """The film is complete once the last iteration's add is: the first context's stream waits for
+        it (the frame's collective runs on the current stream after this)."""
         import torch
 
-        if len(self.films) > 1:
-            st0 = self.ctxs[0][1]
-            for _, st in self.ctxs[1:]:
-                st0.wait_stream(st)
-            with torch.cuda.stream(st0):
-                for f in self.films[1:]:
-                    self.films[0].add_(f)
+        if self._last_add is not None:
+            torch.cuda.current_stream().wait_event(self._last_add)
 
     def close(self):
         for c, _ in self.ctxs[1:]:
             c.close()
 
-    def diagnostics(self):
+    def diagnostics(self, k=0):
         import torch
 
-        self.step(0, None, scratch=True)
+        self.step(k, None, scratch=True, ctx=0)  # the first context: the one with the counters on
         self.g.synchronize()
         torch.cuda.synchronize()
         st = self.g.stats()
@@ -701,7 +739,7 @@ class SyntheticWorkload:
             ev[1].record()
         return self.nseg
 
-    def diagnostics(self):
+    def diagnostics(self, k=0):
         self.step(0, None, scratch=True)
         self.g.synchronize()
         st = self.g.stats()

@@ -34,13 +34,14 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
     st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000, "queued_pairs": 500}
     r = bench.roofline(st, a, WL(), 2.0, None, None)
     items = (640 + 63) // 64 * 4
-    # 112 B per queued pair: three SegRec planes, the record carries the power (128 B split layout)
-    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 112.0 * 500 + 640 * 12 * (4 + 1)
-    # without the PMC passes: the HBM roofline of the algorithmic bytes
-    assert r["bound"] == "hbm" and r["hbm"]["algorithmic_bytes_per_launch"] == alg
+    # 48 B per queued pair: three SegRec planes (the beam comes from the tile's LDS planes; + 16 B of
+    # power with the split layout)
+    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 48.0 * 500 + 640 * 12 * (4 + 1)
+    # without the PMC passes: the HBM roofline of the requested bytes
+    assert r["bound"] == "hbm" and r["hbm"]["requested_bytes_per_launch"] == alg
     a_split = bench.parse(["--split", "4", "--split-records", "1"])
     r_split = bench.roofline(st, a_split, WL(), 2.0, None, None)
-    assert r_split["hbm"]["algorithmic_bytes_per_launch"] == alg + 16.0 * 500
+    assert r_split["hbm"]["requested_bytes_per_launch"] == alg + 16.0 * 500
     assert r["achieved"] == pytest.approx(alg / 2e-3 / 1e9)
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) and r["unit"] == "GB/s" and r["traffic"] is None
     # with them: VALU issue binds; frac = instructions / (256 CU x 4 SIMD / 2 x clocks), HBM kept aside
@@ -52,7 +53,9 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
     assert r["peak"] == pytest.approx(512 * 2.0e7 / 1e-2 / 1e9)  # 2 GHz
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"]) == pytest.approx(issue["valu_issue_frac"])
     assert r["hbm"]["traffic_GBps"] == pytest.approx(4.0e9 / 1e-2 / 1e9)
-    assert r["hbm"]["traffic_over_algorithmic"] == pytest.approx(4.0e9 / alg)
+    assert r["hbm"]["traffic_over_requested"] == pytest.approx(4.0e9 / alg)
+    pmc["l2"] = {"TCC_HIT_sum": 3.0, "TCC_MISS_sum": 1.0, "hit_rate": 0.75}
+    assert bench.roofline(st, a, WL(), 2.0, pmc, None)["l2"]["hit_rate"] == 0.75
 
 
 def test_host_threads_positive(bench):
