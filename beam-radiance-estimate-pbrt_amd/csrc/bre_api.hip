@@ -66,7 +66,8 @@ struct bre_ctx {
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
     int tile_axis = 0;       // internal: tile kernel tile axis reject (GatherArgs::tileax), 1 = on (measured slower)
-    int occupancy = 5;       // tile kernel register budget (min waves per SIMD): 5 = the LDS bound of the round-4 tile planes (7.5 KB per wave)
+    int film_compose = 1;    // internal (option 114): 1 = per-pixel deterministic compose (default), 0 = float atomics (A/B)
+    int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
     int shard_rank = 0, shard_count = 1;  // camera-pass image-tile shard of this context
     int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
@@ -696,6 +697,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "record layout must be 0 or 1");
         c->split_records = (int)value;
         return BRE_OK;
+    case 114:  // internal: film accumulation, 1 deterministic per-pixel compose (default) / 0 float atomics (A/B)
+        if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "film mode must be 0 or 1");
+        c->film_compose = (int)value;
+        return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
         c->margin = (int)value;
@@ -1138,7 +1143,7 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
                                   const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
                                   float *d_seg_rgb, int32_t *d_seg_counts) {
     const bool sortable = c->kernel == 0 || c->kernel == 4;
-    if (!d_accum || !sortable || n <= 0 || !pix || c->nvalid == 0)
+    if (!d_accum || !sortable || n <= 0 || !pix || c->nvalid == 0 || !c->film_compose)
         return gather_segments_core(c, n, o, p, d, t, pix, R, npix, d_accum, d_seg_rgb, d_seg_counts);
     const size_t N = (size_t)n;
     float *segbuf = d_seg_rgb;

@@ -140,10 +140,12 @@ __device__ __forceinline__ const float4 *seg_plane(const SegRec *base, int64_t s
 
 // Per leaf tile of the tile kernel's tree, per gather (k_tile_axis): an axis line p + s d (|d| = 1)
 // such that every beam LINE of the tile, clipped to the box of the gather's segments grown by
-// (R + rmax) and a margin, lies within rho of it.  rho < 0: the tile cannot contribute at all.
+// (R + rmax) and a margin, lies within rho of it -- stored as the scan's separable record of a
+// pseudo-beam: d, m = d x p and thr = rho + the beam-side prefilter margin Ab' (maxd = R + rmax);
+// live < 0: no beam of the tile can contribute at all.
 struct alignas(16) TileAxis {
-    float p[3], rho;
-    float d[3], rmax;  // rmax: the tile's largest beam radius
+    float d[3], thr;
+    float m[3], live;
 };
 
 struct GatherArgs {

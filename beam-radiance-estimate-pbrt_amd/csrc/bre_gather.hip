@@ -39,23 +39,24 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
 // tiles not scanned), 5 = exact stage accumulates in one racy RMW round instead of the ordered rank
 // rounds (wrong sums: the price of the ordering).
-// BRE_HOLD 1 (default): queue entries left over at the end of a leaf tile keep their beam in the
-// lanes' registers (HeldBeam) and join the next full exact batch; 0: they run at once as a partial batch
-#ifndef BRE_HOLD
-#define BRE_HOLD 1
+// Exact stage (buffer-load path): 1 = recompute the segment's unit direction instead of loading
+// SegRec plane 2 (default), 0 = load it (A/B)
+#ifndef BRE_AU_RECOMPUTE
+#define BRE_AU_RECOMPUTE 1
 #endif
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
+#endif
+// BRE_RMW_ROUNDS: exact-stage read-modify-write rounds per batch, 64 (default) = every rank in
+// rounds (queue order, documented operations only); < 64 (timing A/B only) adds the ranks beyond
+// by LDS float atomics, whose same-address order within one instruction is not documented
+#ifndef BRE_RMW_ROUNDS
+#define BRE_RMW_ROUNDS 64
 #endif
 // BRE_PHASE_TIMING 1 (profiling builds only): the production tile kernel adds, per wave, the
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
-// BRE_RMW_MAX_RUNS: exact-stage read-modify-write rounds per batch; a segment's pairs beyond this
-// many in one batch accumulate by LDS float atomics (tile_exact)
-#ifndef BRE_RMW_MAX_RUNS
-#define BRE_RMW_MAX_RUNS 64
-#endif
 // BRE_NODE_RELOAD 1: the production instantiation re-reads o, tmax, 1/d from the SegRec at each node
 // visit (register budget, occupancy 7); 0 (default) keeps them in registers at occupancy 6, +1.5% at
 // C2 and C3 once the LPT order made the node loads cheap (explore38)
@@ -74,10 +75,21 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
 #endif
+// BRE_EXACT_SHFL 1: the exact stage takes the pair's segment o, tmax, 1/d, au and has_inf from the
+// segment's own lane by ds_bpermute instead of loading three SegRec planes (texture-path relief)
+#ifndef BRE_EXACT_SHFL
+#define BRE_EXACT_SHFL 0
+#endif
 // BRE_SQRT_NOSCALE 1 (default): the exact stage's two square roots without the compiler's small-input
 // scaling (sqrt_cr_noscale, bit-identical results: see tile_exact); 0 = sqrtf
 #ifndef BRE_SQRT_NOSCALE
 #define BRE_SQRT_NOSCALE 1
+#endif
+// BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes through a buffer descriptor
+// (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer math;
+// with the power too, C2 +0.8%, C3 +2%, profiles/r3b/run4)
+#ifndef BRE_BUF_LOADS
+#define BRE_BUF_LOADS 1
 #endif
 // Raw buffer resource over [p, p + 4 GiB): offsets are 32-bit, out-of-range reads return 0.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *p) {
@@ -339,17 +351,21 @@ __device__ __forceinline__ bool bundle_far_sep(const Bundle &K, f3 b0, f3 bu, f3
 }
 
 // ---------------------------------------------------------------------------------------------
-// Tile axis reject (option 112, OFF by default: measured -2..-3% at C2, +-1% at C3, profiles/r3b/run5-6;
-// the tiles it skips are almost all tiles whose beams the packet rejects anyway, so it saves only
-// their staging, and the per-gather axis pass + per-leaf test cost more).  A contributing pair (lane i, beam j) has the reference's pA on segment i (to
-// rounding) and its pB on beam j's line with |pA - pB| < maxd_j, so pB lies in the box of the
-// launch's segments grown by maxd_j.  If every beam line of a tile, clipped to that box (plus a
-// margin), lies within rho of the tile's axis line (k_tile_axis: distance to a line is convex along
-// a line, so the clipped piece's two end points bound it), then dist(pB, axis) <= rho, while
-// dist(pA, C) <= delta (the packet's bundle line); hence D(C, axis) <= rho + delta + maxd_j for
-// any contributing pair, and a tile with D(C, axis) > rho + delta + maxd_max (+ margins) holds no
-// pair that can contribute to this packet: it is skipped without staging (the production
-// instantiation only: the counting one box-tests every beam of every visited tile for C).
+// Per-lane tile line reject (option 112 = 1).  A contributing pair (lane i, beam j) has the reference's
+// pA on segment i (to rounding) and pB on beam j's line with |pA - pB| < maxd_j, so pB lies in the box
+// of the launch's segments grown by maxd_j.  k_tile_axis gives every tile an axis line such that every
+// beam LINE of the tile, clipped to that box (plus a margin), lies within rho of it (distance to a line
+// is convex along a line, so the clipped piece's two end points bound it).  Then
+//   D(line_i, axis) <= d(pA, axis) <= |pA - pB| + d(pB, axis) < maxd_j + rho,
+// so a lane whose segment LINE is farther than rho + maxd_max from the axis line has no pair in the
+// tile that can contribute.  The test is the scan's own separable line-distance test
+// (scan_keep_mask) with the axis as a pseudo-beam whose threshold is rho + Ab' (Ab' with the tile's
+// largest |b0|_1 and |B|, so the scan's rounding analysis covers every beam of the tile): per leaf
+// visit one 14-VALU test per lane, before the tile is staged.  Lanes it rejects are taken off the tile
+// (fewer lanes on: more tiles take the transposed scan), and a tile no lane keeps is not staged at all.
+// Only the production instantiation tests (the counting one box-tests every beam of a visited tile for
+// C); the rejected pairs never contribute, so the queues differ only by non-contributing pairs and
+// every per-segment sum is bit-identical (tests/test_prefilter_options_gpu.py).
 __device__ __forceinline__ unsigned int ord_u(float f) {
     const unsigned int u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -399,7 +415,8 @@ __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__res
 }
 
 // One wave per leaf tile: axis = mean start -> mean end of its usable beams, rho = the largest
-// distance of a clipped beam line's end points from the axis (with rounding margins).
+// distance of a clipped beam line's end points from the axis (with rounding margins), stored as the
+// pseudo-beam record the per-lane tile line reject tests (TileAxis).
 __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ recs, BeamSet bset, int64_t nvalid,
                                                   int leaf_size,
                                                   const unsigned int *__restrict__ segb, float R,
@@ -425,11 +442,11 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
     TileAxis A;
     if (n == 0.f || !(segb[0] <= segb[3] && segb[1] <= segb[4] && segb[2] <= segb[5])) {
         // no usable beam (or no finite segment): nothing of this tile can contribute
-        A.p[0] = A.p[1] = A.p[2] = 0.f;
         A.d[0] = 1.f;
         A.d[1] = A.d[2] = 0.f;
-        A.rho = -1.f;
-        A.rmax = rmax;
+        A.thr = 0.f;
+        A.m[0] = A.m[1] = A.m[2] = 0.f;
+        A.live = -1.f;
         if (lane == 0) out[tile] = A;
         return;
     }
@@ -482,31 +499,25 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
             if (!(dist == dist)) dist = FLT_MAX;
         }
     }
-    const float rho = wave_max(dist);
+    const float rho_raw = wave_max(dist);
     const float pm = fmaxf(fmaxf(fabsf(ps.x), fabsf(ps.y)), fabsf(ps.z));
-    A.p[0] = ps.x;
-    A.p[1] = ps.y;
-    A.p[2] = ps.z;
+    const float rho = rho_raw * 1.0001f + 1e-5f * (cm + pm + grow) + 1e-6f;
+    // the scan's beam-side margin Ab' (make_scan_beam) with maxd_max and the tile's largest |b0|_1 and
+    // |B| (the separable form evaluates t.n at the axis point: its |p|_1 joins the max)
+    const float b1 = wave_max(ok ? fabsf(b0.x) + fabsf(b0.y) + fabsf(b0.z) : 0.f);
+    const float p1 = fabsf(ps.x) + fabsf(ps.y) + fabsf(ps.z);
+    const float bmag = wave_max(ok ? mb : 0.f);
+    const float ab = (R + rmax) * 1.000001f + 1.93e-5f * fmaxf(b1, p1) + 2.4e-7f * bmag + 1e-6f;
+    const float thr = (rho + ab) * 1.0001f + 1e-6f;
     A.d[0] = d.x;
     A.d[1] = d.y;
     A.d[2] = d.z;
-    A.rho = rho * 1.0001f + 1e-5f * (cm + pm + grow) + 1e-6f;
-    A.rmax = rmax;
+    A.thr = (rho_raw < FLT_MAX && isfinite(thr)) ? thr : FLT_MAX;  // FLT_MAX: never a reject
+    A.m[0] = d.y * ps.z - d.z * ps.y;  // m = d x p (the scan's m0 = bu x b0)
+    A.m[1] = d.z * ps.x - d.x * ps.z;
+    A.m[2] = d.x * ps.y - d.y * ps.x;
+    A.live = 1.f;
     if (lane == 0) out[tile] = A;
-}
-
-// D(C, axis) > rho + delta + maxd_max + margins (all wave-uniform).  Near-parallel axes (|n|^2 <
-// 1e-4, where the float cross product is too inexact to divide by) are never skipped.
-__device__ __forceinline__ bool tile_axis_far(const Bundle &K, const TileAxis *__restrict__ tax, int64_t tile, float R) {
-    const float4 *q = reinterpret_cast<const float4 *>(tax + tile);
-    const float4 a = q[0], b = q[1];
-    const f3 n = mk(K.cu.y * b.z - K.cu.z * b.y, K.cu.z * b.x - K.cu.x * b.z, K.cu.x * b.y - K.cu.y * b.x);
-    const float nn = lensq3(n);
-    const f3 w = mk(a.x - K.co.x, a.y - K.co.y, a.z - K.co.z);
-    const float wn = fabsf(dot3(w, n));
-    const float w1 = fabsf(w.x) + fabsf(w.y) + fabsf(w.z);
-    const float lim = a.w + K.delta + (R + b.w) * 1.001f + 1e-4f * w1 + 1e-5f;
-    return (a.w < 0.f) | ((nn >= 1e-4f) & (K.delta < 1e30f) & (wn > lim * sqrtf(nn) * 1.0001f));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -601,21 +612,21 @@ __device__ __forceinline__ ScanBeam make_scan_beam(const BeamV &r, float R, int 
     return B;
 }
 
-// Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128 of planes 0 and 1):
-// (bu, -) and (m0, thr_sq).  Plane 0's w is the exact stage's power.z; the scan does not use it, but
-// an opaque use keeps the read a ds_read_b128 (a read whose w is unused is narrowed to ds_read_b96:
-// 8 LDS cycles per wave, not 4).
+// Beam j's scan values from the tile staged in LDS (two broadcast ds_read_b128): (bu, thr_sq) and
+// (m0, 1.0001).  The stored constant is the u' constant of scan_need, so every loaded component has
+// a use (a read whose w is unused is narrowed to ds_read_b96: 8 LDS cycles per wave, not 4).
 struct ScanStaged {
     f3 bu, m0;
     float thr_sq;  // fl(thr * |thr|), thr = Ab' + the packet's max Al'; -inf: rejected; +inf: never
+    float uc;      // 1.0001
 };
-__device__ __forceinline__ ScanStaged scan_beam_lds(const float4 (*tb)[64], int j) {
-    const float4 a = tb[0][j], b = tb[1][j];
-    asm volatile("" : : "v"(a.w));
+__device__ __forceinline__ ScanStaged scan_beam_lds(const float4 (*tile)[2], int j) {
+    const float4 a = tile[j][0], b = tile[j][1];
     ScanStaged B;
     B.bu = mk(a.x, a.y, a.z);
-    B.thr_sq = b.w;
+    B.thr_sq = a.w;
     B.m0 = mk(b.x, b.y, b.z);
+    B.uc = b.w;
     return B;
 }
 
@@ -639,7 +650,7 @@ __device__ __forceinline__ ScanStaged scan_beam_lds(const float4 (*tb)[64], int 
 // result mask, combined on the scalar unit (no bool materialisation in VALU).  All lanes must call.
 __device__ __forceinline__ unsigned long long scan_keep_mask(const ScanLane &S, f3 au, const ScanStaged &B) {
     const float c = __builtin_fmaf(au.x, B.bu.x, __builtin_fmaf(au.y, B.bu.y, au.z * B.bu.z));
-    const float u = __builtin_fmaf(-c, c, 1.0001f);
+    const float u = __builtin_fmaf(-c, c, B.uc);
     const float x = __builtin_fmaf(au.x, B.m0.x, __builtin_fmaf(au.y, B.m0.y, au.z * B.m0.z));
     const float t = __builtin_fmaf(-B.bu.x, S.q.x, __builtin_fmaf(-B.bu.y, S.q.y, __builtin_fmaf(-B.bu.z, S.q.z, x)));
     return ~(__ballot(u >= 0.0101f) & __ballot((t * t) > B.thr_sq * u));
@@ -648,166 +659,88 @@ __device__ __forceinline__ unsigned long long scan_keep_mask(const ScanLane &S, 
 constexpr int kTileBlock = 64;   // one wave per workgroup: a finished wave frees its slot at once
 constexpr int kQueueCap = 192;   // >= 63 left over + 128 appended by one scan step (two beams)
 
-// One queued (beam, lane) pair, 16 bits: the beam's index in the current leaf tile (bits 0-5) and the
-// segment's lane (bits 6-11).  Entries of an earlier tile are resolved into registers (HeldBeam)
-// before the tile's LDS planes are overwritten.
-__device__ __forceinline__ unsigned int qentry(int beam, int lane) { return (unsigned int)beam | ((unsigned int)lane << 6); }
+// One queued (beam, lane) pair: the beam's index in BVH order and the segment's lane.
+struct QEntry {
+    int32_t beam;
+    int32_t lane;
+};
 
-// The current leaf tile in LDS, plane-major (plane k of beam j at tb[k][j], 1 KB per plane; the exact
-// stage reads planes 0, 2, 3 and 4 whole, four ds_read_b128):
-//   0 (bu, p.z)               scan (bu), exact (bu; p.z: the power's third channel of a uniform-radius set)
-//   1 (m0, thr_sq)            scan
-//   2 (lo.xyz, hi.x)          exact: the beam's (group) box
-//   3 (hi.yz, b0.xy)          exact
-//   4 (b0.z, |B|, p.x, p.y)   exact; a mixed-radius set: (b0.z, |B|, radius, -), power from `pow`
-// The exact stage reads its beam from here (four ds_read_b128 + one ds_read_b32) instead of the
-// 64-B BeamRec line through the texture path (the vector-memory data return was the
-// kernel's busiest unit; the beam line was four of the seven 16-B loads of every queued pair).
 struct TileShared {
-    float4 tb[5][64];
-    float4 acc[64];                 // per-segment RGB sums and contribution count (w, exact below 2^24)
-    unsigned long long rkm[64];     // exact batch: per-segment masks of its contributing positions
-    uint16_t q[kQueueCap + 64];     // prefilter survivors [0, t1), then one discard slot per lane
+    float4 tile[64][2];          // scan layout of the current leaf tile: (bu, Ab'), (m0, -)
+    float4 acc[64];              // per-segment RGB sums and contribution count (w, exact below 2^24)
+    unsigned long long rkm[64];  // exact batch: per-segment masks of its contributing positions (rank)
+    QEntry q[kQueueCap + 64];    // prefilter survivors [0, t1), then one discard slot per lane
     int32_t stk[kStackDepth];
 };
 
-// The beam of queue position p (p < nheld) of an EARLIER tile, held in lane p's registers from the
-// moment that tile's planes are replaced until the next exact batch consumes it: planes 0 (w: p.z;
-// a mixed-radius set: the beam's index bits), 2, 3 and 4.
-struct HeldBeam {
-    float p0x, p0y, p0z, p0w, p2x, p2y, p2z, p2w, p3x, p3y, p3z, p3w, p4x, p4y, p4z, p4w;  // scalars: SROA-friendly
-    __device__ __forceinline__ void set(float4 a0, float4 a2, float4 a3, float4 a4) {
-        p0x = a0.x; p0y = a0.y; p0z = a0.z; p0w = a0.w;
-        p2x = a2.x; p2y = a2.y; p2z = a2.z; p2w = a2.w;
-        p3x = a3.x; p3y = a3.y; p3z = a3.z; p3w = a3.w;
-        p4x = a4.x; p4y = a4.y; p4z = a4.z; p4w = a4.w;
-    }
-};
-
-// Accumulate one batch's pair values v (RGB, w = 1 for a contributing pair) into the segments' LDS
-// sums, deterministically and without relying on how the hardware orders same-address lanes:
-// * rank: every contributing lane ORs its bit into its segment's 64-bit mask (ds_or_b64: OR is
-//   commutative, so the mask does not depend on the order the lanes are applied in), and its rank is
-//   the number of mask bits below it -- its position among its segment's pairs in queue order;
-// * a batch whose most repeated segment has at most BRE_RMW_MAX_RUNS pairs adds in rounds: round k
-//   read-modify-writes the rank-k pairs, whose segments are distinct (one wave's LDS accesses are
-//   performed in order), so each segment adds its pairs in queue order;
-// * a batch with a longer run (a transposed tile, a packet with few lanes on) is permuted by segment
-//   instead -- stable, positions from the masks' counts (ds_permute to lane off[seg] + rank) -- and
-//   each segment's pairs are added by a segmented Hillis-Steele sum in a fixed tree order, then one
-//   read-modify-write per segment.
-// Both are functions of the batch alone: the same queue gives the same bits on every run.
-__device__ __forceinline__ void accumulate_batch(TileShared &sh, int sl, bool contrib, float4 v) {
-    const int lane = threadIdx.x & 63;
-    if (__ballot(contrib) == 0ull) return;
-    if (BRE_ABLATE == 5) {  // timing ablation only: one racy read-modify-write round (sums are wrong)
-        if (contrib) {
-            float4 a = sh.acc[sl];
-            a.x += v.x;
-            a.y += v.y;
-            a.z += v.z;
-            a.w += v.w;
-            sh.acc[sl] = a;
-        }
-        return;
-    }
-    sh.rkm[lane] = 0ull;
-    __builtin_amdgcn_wave_barrier();
-    if (contrib) atomicOr(&sh.rkm[sl], 1ull << lane);
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long mm = sh.rkm[sl];
-    const int rank = contrib ? lanes_below(mm) : 64;
-    if (__ballot(contrib & (rank >= BRE_RMW_MAX_RUNS)) == 0ull) {
-        for (int k = 0; k < BRE_RMW_MAX_RUNS; ++k) {
-            if (__ballot(rank == k) == 0ull) return;
-            if (rank == k) {
-                float4 a = sh.acc[sl];
-                a.x += v.x;
-                a.y += v.y;
-                a.z += v.z;
-                a.w += v.w;
-                sh.acc[sl] = a;
-            }
-        }
-        return;
-    }
-    // sorted by segment: lane s counts segment s's pairs, an exclusive scan over the lanes gives each
-    // segment its first sorted position
-    const int cnt = __popcll(sh.rkm[lane]);
-    int off = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(off, d);
-        if (lane >= d) off += u;
-    }
-    off -= cnt;
-    const unsigned long long cm = __ballot(contrib);
-    const int nc = __popcll(cm);
-    const int seg_off = __builtin_amdgcn_ds_bpermute(sl << 2, off);
-    const int dst = (contrib ? seg_off + rank : nc + lanes_below(~cm)) << 2;  // a permutation of the lanes
-    const int ps = __builtin_amdgcn_ds_permute(dst, contrib ? sl : 64 + lane);  // 64+: never a segment
-    const bool tail = lane < nc && (lane == 63 || __shfl_down(ps, 1) != ps);
-    // one channel at a time (register pressure: this runs inside the scan loop)
-#pragma nounroll
-    for (int ch = 0; ch < 3; ++ch) {
-        const float vc = ch == 0 ? v.x : (ch == 1 ? v.y : v.z);
-        float x = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(vc)));
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const float ux = __shfl_up(x, d);
-            const int us = __shfl_up(ps, d);
-            if (lane >= d && us == ps) x = ux + x;
-        }
-        if (tail) {
-            float *a = reinterpret_cast<float *>(&sh.acc[ps]);
-            a[ch] += x;
-        }
-    }
-    if (tail) sh.acc[ps].w += (float)__popcll(sh.rkm[ps]);
-}
-
 // The exact stage for n queued prefilter survivors q[first, first + n) (one per lane; all lanes
 // call): the reference's box test on the beam's (group) box, then ComputeClosestPoints + kernel.
-// The pair's segment comes from its SegRec (three 16-B loads through a buffer descriptor), the beam
-// from the current tile's LDS planes -- or, for positions below nheld (entries of an earlier tile,
-// only in the first batch after a tile change), from the lane's HeldBeam registers.
-__device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, int nheld, const HeldBeam &hb,
-                                           const SegRec *__restrict__ srec, const float *__restrict__ sd,
-                                           int64_t seg0, const float4 *__restrict__ pw, int64_t tile_first,
-                                           const BeamSet &bset, float R, float inv_maxd) {
+// The pair's segment comes from its SegRec, the beam line from L2.
+__device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, const SegRec *__restrict__ srec,
+                                           const float *__restrict__ sd, int64_t seg0,
+                                           const BeamRec *__restrict__ recs, const float4 *__restrict__ pw,
+                                           const BeamSet &bset, float R, float inv_maxd,
+                                           bool count, const Lane &L) {
     const int lane = threadIdx.x & 63;
     const bool on = lane < n;
-    const unsigned int e = sh.q[first + (on ? lane : 0)];  // off lanes (a partial batch) read a valid entry
-    const int j = (int)(e & 63u), sl = (int)((e >> 6) & 63u);
+    const QEntry e = sh.q[first + (on ? lane : 0)];  // off lanes (a partial batch) read a valid entry
+    const int sl = e.lane;
+    const int64_t b = e.beam;
+    // every load of the pair is issued at once (one memory round trip per batch; most queued pairs
+    // pass the box test, so the second half is rarely wasted)
+    const float4 *sr = seg_plane(srec, seg0 + sl, 0);  // packet-plane layout: plane k at sr[64 k]
+    const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
+#if BRE_EXACT_SHFL
+    // the segment's o, tmax, 1/d (sanitised), au and has_inf are resident in lane sl's registers:
+    // fetched by ds_bpermute (LDS crossbar) instead of three of the four SegRec loads (texture path)
+    (void)sd;
+    const int sa = sl << 2;
+    const auto shf = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(v))); };
+    const float4 s1 = sr[64], bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
+    const float4 s0 = make_float4(shf(L.o.x), shf(L.o.y), shf(L.o.z), shf(L.tmax));
+    const float4 s3 = make_float4(shf(L.invs.x), shf(L.invs.y), shf(L.invs.z), 0.f);
+#if BRE_EXACT_SHFL == 2
+    const float4 s2 = sr[128];  // 2: only the box-test values by ds_bpermute
+#else
+    const float4 s2 = make_float4(shf(L.au.x), shf(L.au.y), shf(L.au.z),
+                                  __int_as_float(__builtin_amdgcn_ds_bpermute(sa, L.has_inf ? 1 : 0)));
+#endif
+#elif BRE_BUF_LOADS
+    (void)L;
+    (void)sr;
     // SegRec plane k of this packet at byte (seg0 / 64) * 4096 + k * 1024 + sl * 16 (packet-plane layout;
-    // one launch's records stay far below 4 GiB: bre_api.hip caps a launch's segments)
+    // one launch's records stay far below 4 GiB: bre_api.hip caps a launch's segments).  The beam
+    // record and power stay 64-bit pointer loads: a beam index may exceed 2^26 (2^28) records of 64
+    // (16) bytes, past a 32-bit byte offset.
     const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec);
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
-    const float4 s0 = buf_f4(srs, vo, so_), s1 = buf_f4(srs, vo + 1024u, so_), s3 = buf_f4(srs, vo + 3072u, so_);
-    // the beam from the tile planes (held lanes read a stale slot and replace it below)
-    float4 a0 = sh.tb[0][j], a2 = sh.tb[2][j], a3 = sh.tb[3][j], a4 = sh.tb[4][j];
-    int64_t gb = tile_first + j;  // the beam's index in BVH order (mixed-radius sets: its power line)
-    if (nheld > 0) {  // wave-uniform: the first batch after a tile change
-        const bool h = lane < nheld;
-        // component-wise selects (a select of whole float4 values turns into a select of their
-        // addresses, which keeps them in scratch memory)
-        a0 = make_float4(h ? hb.p0x : a0.x, h ? hb.p0y : a0.y, h ? hb.p0z : a0.z, h ? hb.p0w : a0.w);
-        a2 = make_float4(h ? hb.p2x : a2.x, h ? hb.p2y : a2.y, h ? hb.p2z : a2.z, h ? hb.p2w : a2.w);
-        a3 = make_float4(h ? hb.p3x : a3.x, h ? hb.p3y : a3.y, h ? hb.p3z : a3.z, h ? hb.p3w : a3.w);
-        a4 = make_float4(h ? hb.p4x : a4.x, h ? hb.p4y : a4.y, h ? hb.p4z : a4.z, h ? hb.p4w : a4.w);
-        if (!bset.uniform && h) gb = (int64_t)(unsigned int)__float_as_uint(hb.p0w);
-    }
-    // a uniform-radius set's power is in the tile (4.zw, 0.w); a mixed set's in the pow array
-    const float4 pv = bset.uniform ? make_float4(a4.z, a4.w, a0.w, 0.f) : pw[gb];
-    // au = (p - o) * (1 / |A|) by load_lane's own operations (bit-identical to SegRec plane 2, not loaded)
-    const f3 au = (s1.w != 0.0f) ? div3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s1.w) : mk(0.f, 0.f, 0.f);
+    const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
+#if BRE_AU_RECOMPUTE
+    // au = (p - o) * (1 / |A|) by load_lane's own operations (bit-identical to plane 2, which is not
+    // loaded): VALU, which has headroom, for one of the pair's eight vector loads (the texture-data
+    // path is the kernel's busiest unit); has_inf from plane 3
+    const float4 s1 = buf_f4(srs, vo + 1024u, so_), bz = rb[2], bw = rb[3];
+    const f3 au_ = (s1.w != 0.0f) ? div3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s1.w) : mk(0.f, 0.f, 0.f);
+    const float4 s2 = make_float4(au_.x, au_.y, au_.z, s3.w);
+#else
+    const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
+#endif
+    // a uniform-radius set's power is in the record's last three words (BeamRec): eight loads per pair
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
+#else
+    (void)L;
+    const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
+    const float4 s1 = sr[64], s2 = sr[128], bz = rb[2], bw = rb[3];
+    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
+#endif
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
     const float tmax = s0.w;
-    const Box6 box{a2.x, a2.y, a2.z, a2.w, a3.x, a3.y};
+    const Box6 box{bx.x, bx.y, bx.z, bx.w, by.x, by.y};
     float te;
     bool hit = on & node_test(box, o, mk(s3.x, s3.y, s3.z), tmax, te);
-    const bool inf = s3.w != 0.f;  // has_inf (integer 1 as float bits: a denormal, never 0)
+    const bool inf = s2.w != 0.f;  // has_inf (integer 1 as float bits: a denormal, never 0)
     if (__ballot(on & inf) != 0ull) {
         if (on & inf) {
             // the rare axis-parallel ray: the literal slab test on its exact 1/d
@@ -822,10 +755,10 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, int
     float4 v = make_float4(0.f, 0.f, 0.f, 1.f);
     bool contrib = false;
     if (hit) {
-        const float maxd = R + beam_radius(bset, a4.z);  // MaxDistance = currentBeamRadius + beam->radius
+        const float maxd = R + beam_radius(bset, bw.y);  // MaxDistance = currentBeamRadius + beam->radius
         float d2, unused;
-        const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), au, s1.w, mk(a3.z, a3.w, a4.x),
-                                                        mk(a0.x, a0.y, a0.z), a4.y, d2, unused);
+        const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w,
+                                                        mk(by.z, by.w, bz.x), mk(bz.y, bz.z, bz.w), bw.x, d2, unused);
         // |pA - pB| correctly rounded (photonbeam.cpp:500).  Without the compiler's small-input scaling
         // when maxd >= 2^-30: for d2 >= 2^-96 the root is bit-identical; below, both roots are < 2^-47.9,
         // so both pass dist < maxd and give r < 2^-17.9, r^2 < 2^-35 and 1 - r^2 == 1: the same value.
@@ -855,7 +788,75 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, int
             contrib = true;
         }
     }
-    accumulate_batch(sh, sl, contrib, v);
+    // Accumulate into the segments' LDS sums in queue order, deterministically and without relying on
+    // how the hardware orders same-address lanes of one instruction.  A pair's rank is the number of
+    // its segment's contributing pairs below it in the batch (the mask bits below its lane): its
+    // position among its segment's pairs in queue order.  Round k read-modify-writes the contributing rank-k
+    // pairs, whose segments are distinct; one wave's LDS accesses are performed in order, so every
+    // segment adds its terms in queue order.  A batch takes as many rounds as its most repeated segment
+    // has pairs (up to 64 for a transposed tile's segment); round 3 took its ranks from ds_add_rtn_u32
+    // and added ranks >= 8 by LDS float atomics, both of whose same-address orders within one
+    // instruction are undocumented.  (`count` only decides whether the count is used: it is always kept.)
+    (void)count;
+    if (__ballot(contrib) == 0ull) return;
+    if (BRE_ABLATE == 5) {  // timing ablation only: one racy read-modify-write round (sums are wrong)
+        if (contrib) {
+            float4 a = sh.acc[sl];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+            sh.acc[sl] = a;
+        }
+        return;
+    }
+    // rank: every contributing lane ORs its bit into its segment's 64-bit mask with ds_or_rtn_b64, which
+    // returns the mask as it was before this lane's OR.  Whatever order the hardware applies one
+    // instruction's same-address lanes in, a lane's returned mask holds only lanes of its own segment;
+    // if every returned mask holds only LOWER lanes, each segment's lanes were applied in ascending lane
+    // order and the returned bit count is the lane's position among its segment's pairs in queue order.
+    // That is checked (one ballot); a batch that fails it (never observed) takes its ranks from the
+    // final masks instead, after the ORs.  Either way the rank is the lane-order position: the sums
+    // are the same bits whatever the hardware's order.
+    sh.rkm[lane] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long lane_bit = 1ull << lane;
+    unsigned long long before = 0ull;
+    if (contrib) before = atomicOr(&sh.rkm[sl], lane_bit);
+    int rank = contrib ? __popcll(before) : 64;
+    if (__ballot(contrib && (before & ~(lane_bit - 1ull)) != 0ull) != 0ull) {
+        __builtin_amdgcn_wave_barrier();
+        rank = contrib ? lanes_below(sh.rkm[sl]) : 64;
+    }
+    // ranks are dense per segment (0 .. its count - 1): the first rank level no lane holds ends the rounds
+    const auto round_k = [&](int k) {
+        if (rank == k) {
+            float4 a = sh.acc[sl];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+            sh.acc[sl] = a;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (__ballot(rank == k) == 0ull) return;
+        round_k(k);
+    }
+    // a segment repeated more than 8 times in the batch (a transposed tile, few lanes on): the further
+    // rounds, in a loop (BRE_RMW_ROUNDS < 64, timing A/B only: LDS float atomics, undocumented order)
+#pragma nounroll
+    for (int k = 8; k < BRE_RMW_ROUNDS; ++k) {
+        if (__ballot(rank == k) == 0ull) return;
+        round_k(k);
+    }
+    if (BRE_RMW_ROUNDS < 64 && contrib && rank >= BRE_RMW_ROUNDS) {
+        atomicAdd(&sh.acc[sl].x, v.x);
+        atomicAdd(&sh.acc[sl].y, v.y);
+        atomicAdd(&sh.acc[sl].z, v.z);
+        atomicAdd(&sh.acc[sl].w, v.w);
+    }
 }
 
 // COUNT: also box-test every beam of every visited tile and count the candidates (the reference's
@@ -919,21 +920,17 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     unsigned long long visits = 0;
     Prof pf;
     int t1 = 0;                // wave-uniform queue length: survivors in q[0, t1)
-    int nheld = 0;             // wave-uniform: q[0, nheld) are entries of an earlier tile, held in hb
-    HeldBeam hb;
-    hb.set(make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f),
-           make_float4(0.f, 0.f, 0.f, 0.f));
     int64_t cur_first = 0;     // first beam of the current leaf
     unsigned long long ph_stage = 0, ph_scan = 0, ph_exact = 0;
     unsigned long long ss_on = 0, ss_kept = 0, ss_steps = 0, ss_pairs = 0, ss_leaves = 0, ss_q = 0, ss_min = 0,
                        ss_tr = 0;
     const unsigned long long ph_t0 = phase_clock();
 
-    // queue the (beam, lane) survivors of one scan test, in lane order: every lane stores (branch-
-    // free), a lane that queues nothing into its own discard slot (m: the wave-uniform lane mask of
-    // the entries to queue; e: this lane's entry)
+    // queue the (beam, lane) survivors of beam j of the current leaf, in lane order: every lane
+    // stores (branch-free), a lane that queues nothing into its own discard slot
+    // (m: the wave-uniform lane mask of the entries to queue)
     const int discard = kQueueCap + lane;
-    const auto push = [&](unsigned long long m, unsigned int e) {
+    const auto push = [&](unsigned long long m, int32_t e_beam, int32_t e_lane) {
         if (m == 0ull) return;
         int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)t1));
@@ -942,7 +939,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // (inverse ballot): one v_cndmask, every lane stores
         asm volatile("" : "+v"(rank));
         const int slot = __builtin_amdgcn_inverse_ballot_w64(m) ? rank : discard;
-        sh.q[slot] = (uint16_t)e;
+        sh.q[slot] = QEntry{e_beam, e_lane};
         t1 += __popcll(m);
         if (count_c) pf.queued += __popcll(m);  // the production queue too, when counting contributions
         if (BRE_SCAN_STATS) ss_q += __popcll(m);
@@ -956,15 +953,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         int h = 0;
         while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2)
-                tile_exact(sh, h, 64, h == 0 ? nheld : 0, hb, srec, sd, seg0, pw, cur_first, bset, R, inv_maxd);
+            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
             h += 64;
             __builtin_amdgcn_wave_barrier();
         }
-        nheld = 0;
         const int rest = t1 - h;  // h >= 64 > rest: source and destination do not overlap
         if (rest > 0) {
-            uint16_t e = 0;
+            QEntry e{0, 0};
             if (lane < rest) e = sh.q[h + lane];
             __builtin_amdgcn_wave_barrier();
             if (lane < rest) sh.q[lane] = e;
@@ -974,11 +969,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         if (BRE_PHASE_TIMING) ph_exact += phase_clock() - d0;
     };
 
-    // scan one leaf tile (<= 64 beams): lane j stages beam j's scan values and exact-stage planes in
-    // LDS; bundle rejects; per lane the separable prefilter on the kept beams; survivors queue for the
-    // exact stage
+    // scan one leaf tile (<= 64 beams): lane j stages beam j's scan values in LDS; bundle rejects;
+    // per lane the separable prefilter on the kept beams; survivors queue for the exact stage
     const auto leaf = [&](int32_t c, unsigned long long onm) {
-        const bool lane_on = ((onm >> lane) & 1ull) != 0ull;
+        bool lane_on = ((onm >> lane) & 1ull) != 0ull;
         const int64_t first = (int64_t)(~c) * leaf_size;
         const int nb = (int)min((int64_t)leaf_size, nvalid - first);
         if (COUNT) {
@@ -987,29 +981,29 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         }
         if (BRE_ABLATE == 4) return;
         if (!COUNT && tax != nullptr) {
-            // skip the tile when no pair of it can contribute to this packet (tile_axis_far)
-            if (__builtin_amdgcn_readfirstlane((int)tile_axis_far(K, tax, (int64_t)(~c), R))) {
-                return;
-            }
+            // the per-lane tile line reject: lanes whose segment line is too far from the tile's axis
+            // line leave the tile; a tile no lane keeps is skipped before it is staged
+            const float4 *tq = reinterpret_cast<const float4 *>(tax + (int64_t)(~c));
+            const float4 ta = tq[0], tb = tq[1];
+            if (tb.w < 0.f) return;
+            ScanStaged A;
+            A.bu = mk(ta.x, ta.y, ta.z);
+            A.m0 = mk(tb.x, tb.y, tb.z);
+            const float thr = ta.w + al_max;
+            A.thr_sq = thr < FLT_MAX ? thr * thr : INFINITY;
+            A.uc = 1.0001f;
+            onm &= scan_keep_mask(SL, L.au, A);
+            if (onm == 0ull) return;
+            lane_on = ((onm >> lane) & 1ull) != 0ull;
         }
         const unsigned long long l0 = phase_clock();
+        cur_first = first;
         ScanBeam T;
         T.bu = T.m0 = mk(0.f, 0.f, 0.f);
         T.ab = 0.f;
         bool keep = false;
-        float4 rx = make_float4(0.f, 0.f, 0.f, 0.f), ry = rx, rz = rx, rw = rx;  // the 64-B BeamRec
         if (lane < nb) {
-            const float4 *rq = reinterpret_cast<const float4 *>(recs + first + lane);
-            rx = rq[0];
-            ry = rq[1];
-            rz = rq[2];
-            rw = rq[3];
-            BeamV r;  // load_beam's fields
-            r.box = Box6{rx.x, rx.y, rx.z, rx.w, ry.x, ry.y};
-            r.b0 = mk(ry.z, ry.w, rz.x);
-            r.bu = mk(rz.y, rz.z, rz.w);
-            r.mag_b = rw.x;
-            r.radius = beam_radius(bset, rw.y);
+            const BeamV r = load_beam(recs, first + lane, bset);
             T = make_scan_beam(r, R, margin);
             // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
             // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
@@ -1021,36 +1015,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
         __builtin_amdgcn_wave_barrier();  // the previous tile's reads are done
-        // queue entries [nheld, t1) still name beams of the tile about to be replaced: lane p resolves
-        // position p's beam into its registers (the exact batch that consumes it takes it from there)
-        if (!BRE_HOLD && t1 > 0) {
-            // BRE_HOLD 0: the left-over entries of the tile run now, as a partial batch
-            if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, 0, t1, 0, hb, srec, sd, seg0, pw, cur_first, bset, R, inv_maxd);
-            t1 = 0;
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (BRE_HOLD && t1 > nheld) {
-            if (lane >= nheld && lane < t1) {
-                const int jo = (int)(sh.q[lane] & 63u);
-                const float4 o0 = sh.tb[0][jo];
-                const float oz = bset.uniform ? o0.w : __uint_as_float((unsigned int)(cur_first + jo));
-                hb.set(make_float4(o0.x, o0.y, o0.z, oz), sh.tb[2][jo], sh.tb[3][jo], sh.tb[4][jo]);
-            }
-            nheld = t1;
-            __builtin_amdgcn_wave_barrier();
-        }
-        cur_first = first;
         // every lane writes (the transposed scan reads record `lane`): thr_sq = -inf for a beam the
-        // packet rejects or past the tile's end (bu = m0 = 0), which scan_keep_mask rejects unless the
-        // pair is near-parallel (the pushes mask with km); +inf with the prefilter off (never a reject)
+        // packet rejects or past the tile's end (bu = m0 = 0), which scan_need always rejects; +inf
+        // with the prefilter off (never a reject)
         const float thr = T.ab + al_max;
         const float thr_sq = !keep ? -INFINITY : (prefilter ? thr * fabsf(thr) : INFINITY);
-        sh.tb[0][lane] = make_float4(T.bu.x, T.bu.y, T.bu.z, rw.w);
-        sh.tb[1][lane] = make_float4(T.m0.x, T.m0.y, T.m0.z, thr_sq);
-        sh.tb[2][lane] = rx;
-        sh.tb[3][lane] = ry;
-        sh.tb[4][lane] = make_float4(rz.x, rw.x, rw.y, rw.z);
+        sh.tile[lane][0] = make_float4(T.bu.x, T.bu.y, T.bu.z, thr_sq);
+        sh.tile[lane][1] = make_float4(T.m0.x, T.m0.y, T.m0.z, 1.0001f);
         __builtin_amdgcn_wave_barrier();
         if (COUNT) {
             pf.useful += __popcll(km);
@@ -1058,16 +1029,15 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             // prefilters drop; the queue gets exactly the production survivors, in order
             for (int j = 0; j < nb; ++j) {
                 const bool kept = (km >> j) & 1ull;
-                const unsigned long long mk_ = scan_keep_mask(SL, L.au, scan_beam_lds(sh.tb, j)) & onm;
+                const unsigned long long mk_ = scan_keep_mask(SL, L.au, scan_beam_lds(sh.tile, j)) & onm;
                 const bool need = kept && ((mk_ >> lane) & 1ull);
-                const float4 b2 = sh.tb[2][j], b3 = sh.tb[3][j];
-                const Box6 box{b2.x, b2.y, b2.z, b2.w, b3.x, b3.y};
+                const Box6 box = load_beam(recs, first + j, bset).box;
                 float te;
                 bool hit = lane_on & node_test(box, L.o, L.invs, L.tmax, te);
                 if (L.has_inf) hit = lane_on & slab_test(box, L.o, L.inv, L.n0, L.n1, L.n2, L.tmax, nullptr);
                 cand += hit;
                 pf.rejects += hit & !need;
-                if (kept) push(mk_, qentry(j, lane));
+                if (kept) push(mk_, (int32_t)(cur_first + j), lane);
                 drain();
             }
             return;
@@ -1079,8 +1049,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         // against all kept beams at once (lane j: beam j), so a tile costs min(on lanes, kept beams)
         // steps.  Segment i's pairs are queued in beam order, exactly the order the beam-major scan
         // gives them, and every sum is a per-segment sum in queue order: bit-identical results.  The
-        // batches then hold long stretches of one segment, whose ranks >= BRE_RMW_MAX_RUNS the exact
-        // stage adds by LDS atomics, in queue order like its rounds.
+        // batches then hold long stretches of one segment, which the exact stage adds in as many
+        // read-modify-write rounds, in queue order.
         const bool transposed = tscan > 0 && __popcll(onm) * 8 < __popcll(km) * tscan;
         if (BRE_SCAN_STATS) {
             const unsigned long long on = __popcll(onm), kp = __popcll(km);
@@ -1104,7 +1074,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i), readlane_f(L.au.z, i));
                 // & km: a beam the packet rejected (thr_sq = -inf) still passes scan_keep_mask when it
                 // is near-parallel to segment i (u < 0.0101); the beam-major scan never visits it
-                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tb, lane)) & km, qentry(lane, i));
+                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tile, lane)) & km, (int32_t)(cur_first + lane), i);
                 drain();
             }
             if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
@@ -1119,14 +1089,14 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             const bool two = todo != 0ull;
             const int j2 = two ? __ffsll((long long)todo) - 1 : j1;
             if (two) todo &= todo - 1ull;
-            const ScanStaged B1 = scan_beam_lds(sh.tb, j1), B2 = scan_beam_lds(sh.tb, j2);
+            const ScanStaged B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
             // lane masks: every lane evaluates both tests, the lanes off the tile are masked out
             const unsigned long long n1 =
                 (BRE_ABLATE == 3 ? __ballot(((j1 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B1)) & onm;
             const unsigned long long n2 =
                 (BRE_ABLATE == 3 ? __ballot(((j2 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B2)) & onm;
-            push(n1, qentry(j1, lane));
-            if (two) push(n2, qentry(j2, lane));
+            push(n1, (int32_t)(cur_first + j1), lane);
+            if (two) push(n2, (int32_t)(cur_first + j2), lane);
             drain();
         }
         if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
@@ -1241,10 +1211,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            tile_exact(sh, 0, t1, nheld, hb, srec, sd, seg0, pw, cur_first, bset, R, inv_maxd);
+            tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
         }
         t1 = 0;
-        nheld = 0;
     }
     __builtin_amdgcn_wave_barrier();
     if (valid) {

@@ -15,6 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
 sc = importlib.import_module("beam-radiance-estimate-pbrt_amd.scene")
 args = sys.argv[1:]
+opts = [tuple(int(v) for v in a[4:].split("=")) for a in args if a.startswith("opt:")]  # opt:112=1
+args = [a for a in args if not a.startswith("opt:")]
 wl = "c2"
 if args and args[0] in ("c2", "c3"):
     wl = args.pop(0)
@@ -30,6 +32,8 @@ out = {}
 for it in its:
     R = bre.beam_radius_at(0.01, 0.5, it)
     with bre.BeamGather(0, timing=True) as g:
+        for k, v in opts:
+            g.set_option(k, v)
         g.trace_photons(scene, NPH, it, 5, R)
         g.camera_pass(scene, RES, RES, it, 5, True, True)
         ld = torch.zeros((RES * RES, 3), dtype=torch.float32, device="cuda")
