@@ -65,7 +65,7 @@ struct bre_ctx {
     int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
-    int tile_axis = 0;       // internal: tile kernel tile axis reject (GatherArgs::tileax), 1 = on (measured slower)
+    int tile_axis = 1;       // internal (option 112): per-lane tile line reject (GatherArgs::tileax), 1 = on (default since round 4), 0 = off
     int film_compose = 1;    // internal (option 114): 1 = per-pixel deterministic compose (default), 0 = float atomics (A/B)
     int occupancy = 6;       // tile kernel register budget (min waves per SIMD): 6 with the lane ray in registers (r2 final, 77 VGPRs; explore38)
     int sort_key = 4;        // segment coherence sort key (SegSort::key_mode; 4 measured best at C2)
@@ -488,6 +488,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, c->tileax.ensure(sizeof(TileAxis) * (size_t)ntiles));
         HIPCHK(c, c->segbox.ensure(sizeof(unsigned int) * 8));
         a.tileax = c->tileax.as<TileAxis>();
+        a.tile_local = c->tile_axis == 1 ? 1 : 0;
         a.segbox = c->segbox.as<unsigned int>();
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -688,8 +689,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
         c->tscan = (int)value;
         return BRE_OK;
-    case 112:  // internal: tile kernel tile axis reject, 1 on / 0 off (default; A/B)
-        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0 or 1");
+    case 112:  // internal: per-lane tile line reject, 1 on (default) / 0 off / 2 region-wide threshold only (A/B)
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0, 1 or 2");
         c->tile_axis = (int)value;
         return BRE_OK;
     case 113:  // internal: beam record layout, 0 power in the record for uniform-radius sets (default)

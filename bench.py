@@ -31,7 +31,7 @@ Also reported (rank 0, N = 1):
   path); `traffic` = HBM bytes per
   launch from the same passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE).  `hbm`: the
   requested bytes per launch (node and beam lines of the visited tiles, the segments, the exact
-  stage's 48 B of SegRec per queued pair, the partial sums; counted live by the counter pass) / the launch's
+  stage's 112 B per queued pair, the partial sums; counted live by the counter pass) / the launch's
   HIP-event time against 8 TB/s, and the measured HBM traffic against it.  Without rocprofv3 the
   line falls back to `bound` "hbm" on the requested bytes.  The SURVEY §8d reference-tree byte
   model is kept as `ref_model_*` (not a fraction: one staged beam line feeds 64 lanes).
@@ -93,7 +93,7 @@ def parse(argv=None):
     ap.add_argument("--tscan", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--beam-key", type=int, default=-1, help=argparse.SUPPRESS)  # tree build key study (option 110)
     ap.add_argument("--margin", type=int, default=-1, help=argparse.SUPPRESS)  # prefilter margin A/B (option 111)
-    ap.add_argument("--tile-axis", type=int, default=-1, help=argparse.SUPPRESS)  # tile axis reject A/B (option 112)
+    ap.add_argument("--tile-axis", type=int, default=-1, help=argparse.SUPPRESS)  # tile line reject A/B (option 112)
     ap.add_argument("--split-records", type=int, default=-1, help=argparse.SUPPRESS)  # BeamRec layout A/B (option 113)
     ap.add_argument("--film-compose", type=int, default=-1, help=argparse.SUPPRESS)  # film accumulation A/B (option 114)
     ap.add_argument("--pipeline", type=int, default=1,
@@ -388,11 +388,12 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     # what the packet algorithm requests from the memory hierarchy per launch (L1 / TA level): every
     # visited node line and staged beam line (64 B each) of every (packet, subtree) item; per item the
     # segments (40 B in) and the per-subtree partial sums (12 B out) of its 64 lanes; per queued
-    # (lane, beam) pair the exact stage's three 16-B SegRec planes (48 B: since round 4 the beam comes
-    # from the tile's LDS planes, and the unit direction is recomputed; + 16 B power of a mixed-radius
-    # set); and the reduce (12 B x split in, 12 B out per segment)
+    # (lane, beam) pair the exact stage's loads (three of the segment's 16-B SegRec planes -- the unit
+    # direction is recomputed -- and the 64-B BeamRec, which carries the power of the photon pass's
+    # uniform-radius beams: 112 B; 128 B with the split layout, option 113); and the reduce (12 B x
+    # split in, 12 B out per segment)
     queued = st.get("queued_pairs", 0)
-    pair_b = 64.0 if args.split_records == 1 else 48.0
+    pair_b = 128.0 if args.split_records == 1 else 112.0
     req = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + pair_b * queued
            + nseg * 12 * (args.split + 1))
     requested = req / (gather_ms * 1e-3) / 1e9

@@ -34,9 +34,8 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
     st = {"n_segments": 640, "node_visits": 1000, "beam_evals": 3000, "queued_pairs": 500}
     r = bench.roofline(st, a, WL(), 2.0, None, None)
     items = (640 + 63) // 64 * 4
-    # 48 B per queued pair: three SegRec planes (the beam comes from the tile's LDS planes; + 16 B of
-    # power with the split layout)
-    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 48.0 * 500 + 640 * 12 * (4 + 1)
+    # 112 B per queued pair: three SegRec planes, the record carries the power (128 B split layout)
+    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 112.0 * 500 + 640 * 12 * (4 + 1)
     # without the PMC passes: the HBM roofline of the requested bytes
     assert r["bound"] == "hbm" and r["hbm"]["requested_bytes_per_launch"] == alg
     a_split = bench.parse(["--split", "4", "--split-records", "1"])
