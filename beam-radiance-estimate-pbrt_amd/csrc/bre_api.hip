@@ -488,7 +488,6 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, c->tileax.ensure(sizeof(TileAxis) * (size_t)ntiles));
         HIPCHK(c, c->segbox.ensure(sizeof(unsigned int) * 8));
         a.tileax = c->tileax.as<TileAxis>();
-        a.tile_local = c->tile_axis == 1 ? 1 : 0;
         a.segbox = c->segbox.as<unsigned int>();
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -689,7 +688,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
         c->tscan = (int)value;
         return BRE_OK;
-    case 112:  // internal: per-lane tile line reject, 1 on (default) / 0 off / 2 region-wide threshold only (A/B)
+    case 112:  // internal: per-lane tile line reject, 1 on (default) / 0 off (A/B); 2 = 1 (round-4 scripts)
         if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0, 1 or 2");
         c->tile_axis = (int)value;
         return BRE_OK;

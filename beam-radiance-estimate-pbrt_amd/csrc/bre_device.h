@@ -146,10 +146,6 @@ __device__ __forceinline__ const float4 *seg_plane(const SegRec *base, int64_t s
 struct alignas(16) TileAxis {
     float d[3], thr;
     float m[3], grow;  // grow: the region's growth maxd_max + margins; < 0: no beam of the tile can contribute
-    // the packet-local bound (round 4): the offset of beam line j from the axis at axis parameter s is
-    // affine in s, so every beam line lies within a + b |s - s_m| of the axis there; a packet whose box
-    // (grown by `grow`) projects onto [s_lo, s_hi] tests its lanes against a + b max|s - s_m| (+ Ab')
-    float s_m, a, b, pd;  // pd = p . d (s of a point x is x . d - pd); b = +inf: no local bound
 };
 
 struct GatherArgs {
@@ -182,7 +178,6 @@ struct GatherArgs {
     int tscan;             // tile kernel: transposed scan when on-lanes * 8 < kept beams * tscan (0: off)
     int margin;            // tile kernel prefilter margins: 1 = the tight bound (default), 0 = round 2's
     TileAxis *tileax;      // tile kernel: per-tile axis bounds (ntiles), null = no tile axis reject
-    int tile_local = 1;    // tile line reject: 1 = with the packet-local threshold, 0 = region-wide only (A/B)
     unsigned int *segbox;  // tile kernel: 6 ordered uints of scratch (the launch's segment box)
 };
 

@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__res
 // pseudo-beam record the per-lane tile line reject tests (TileAxis).
 __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ recs, BeamSet bset, int64_t nvalid,
                                                   int leaf_size,
-                                                  const unsigned int *__restrict__ segb, float R, int local,
+                                                  const unsigned int *__restrict__ segb, float R,
                                                   TileAxis *__restrict__ out) {
     const int64_t tile = blockIdx.x;
     const int lane = threadIdx.x;
@@ -459,8 +459,6 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
         A.thr = 0.f;
         A.m[0] = A.m[1] = A.m[2] = 0.f;
         A.grow = -1.f;
-        A.s_m = A.a = A.pd = 0.f;
-        A.b = INFINITY;
         if (lane == 0) out[tile] = A;
         return;
     }
@@ -530,36 +528,7 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
     A.m[0] = d.y * ps.z - d.z * ps.y;  // m = d x p (the scan's m0 = bu x b0)
     A.m[1] = d.z * ps.x - d.x * ps.z;
     A.m[2] = d.x * ps.y - d.y * ps.x;
-    // the packet-local bound.  The point of beam line j whose axis parameter is s, P_j(s) = b0_j + u_j
-    // (s - s0_j) / c_j (s0_j = (b0_j - p) . d, c_j = u_j . d), is offset from the axis point p + d s by
-    // o_j(s) = (b0_j - p) - d s + u_j (s - s0_j) / c_j, affine in s with slope v_j = u_j / c_j - d; so
-    // |o_j(s)| <= |o_j(s_m)| + |v_j| |s - s_m| (triangle inequality), and a beam point pB whose axis
-    // parameter lies in [s_lo, s_hi] is within a + b max(|s_lo - s_m|, |s_hi - s_m|) of the axis line,
-    // a = max_j |o_j(s_m)|, b = max_j |v_j|.  A beam within ~78 degrees of perpendicular to the axis
-    // (|c_j| < 0.2) makes b = +inf: no local bound for the tile (the region-wide rho still holds).
-    const float s0 = dot3(sub3(b0, ps), d), cj = dot3(bu, d);
-    const float s_m = wave_sum(ok ? s0 + 0.5f * mb * cj : 0.f) / n;  // mean axis parameter of the midpoints
-    const bool steep = ok && !(fabsf(cj) >= 0.2f);
-    float oa = 0.f, vb = 0.f;
-    if (ok && !steep) {
-        const float ic = 1.0f / cj;
-        const f3 vj = sub3(scale3(bu, ic), d);
-        const f3 oj = add3(sub3(sub3(b0, ps), scale3(d, s_m)), scale3(bu, (s_m - s0) * ic));
-        oa = sqrtf(lensq3(oj));
-        vb = sqrtf(lensq3(vj));
-        if (!(isfinite(oa) && isfinite(vb))) oa = vb = INFINITY;
-    }
-    const float a_raw = wave_max(oa), b_raw = wave_max(vb);
-    const bool any_steep = __ballot(steep) != 0ull;
-    // rounding: relative 1e-4 on a and b; absolute 1e-5 of the coordinates involved (|p|, |s_m|, the
-    // segment box) on a; the region's growth carries maxd_max and 1e-5 of the box bound for the
-    // projection's rounding
-    const float sa = fabsf(s_m) + pm + cm;
-    A.s_m = s_m;
-    A.a = (a_raw * 1.0001f + 1e-5f * sa + 1e-6f + ab) * 1.0001f + 1e-6f;
-    A.b = (!local || any_steep || !(b_raw < FLT_MAX)) ? INFINITY : b_raw * 1.0001f + 1e-5f;
-    A.pd = dot3(ps, d);
-    A.grow = grow + 1e-5f * (cm + fabsf(A.pd)) + 1e-6f;
+    A.grow = grow;
     if (lane == 0) out[tile] = A;
 }
 
@@ -961,24 +930,6 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     // the largest lane margin Al' of the packet, folded into every beam's threshold at staging (a
     // zero-length segment, Al' = FLT_MAX, is never rejected anyway: see scan_need)
     const float al_max = uniform_f(wave_max(valid && SL.al < FLT_MAX ? SL.al : 0.f));
-    // the packet's box (its segments' end points), for the tile line reject's packet-local threshold;
-    // a non-finite coordinate makes it infinite (the local threshold then never applies)
-    f3 pbox_lo = mk(INFINITY, INFINITY, INFINITY), pbox_hi = mk(-INFINITY, -INFINITY, -INFINITY);
-    if (tax != nullptr && __ballot(valid) != 0ull) {
-        const auto wmin = [&](float v) { return -wave_max(-v); };
-        pbox_lo = mk(uniform_f(wmin(valid ? fminf(L.o.x, L.p.x) : INFINITY)),
-                     uniform_f(wmin(valid ? fminf(L.o.y, L.p.y) : INFINITY)),
-                     uniform_f(wmin(valid ? fminf(L.o.z, L.p.z) : INFINITY)));
-        pbox_hi = mk(uniform_f(wave_max(valid ? fmaxf(L.o.x, L.p.x) : -INFINITY)),
-                     uniform_f(wave_max(valid ? fmaxf(L.o.y, L.p.y) : -INFINITY)),
-                     uniform_f(wave_max(valid ? fmaxf(L.o.z, L.p.z) : -INFINITY)));
-        const bool fin = !valid || (isfinite(L.o.x) && isfinite(L.o.y) && isfinite(L.o.z) && isfinite(L.p.x) &&
-                                    isfinite(L.p.y) && isfinite(L.p.z));
-        if (__ballot(!fin) != 0ull) {
-            pbox_lo = mk(-INFINITY, -INFINITY, -INFINITY);
-            pbox_hi = mk(INFINITY, INFINITY, INFINITY);
-        }
-    }
     // 1 / MaxDistance of a uniform-radius set, correctly rounded, once per wave (tile_exact)
     const float inv_maxd = bset.uniform ? uniform_f(1.0f / (R + bset.radius)) : 0.f;
     sh.acc[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1052,24 +1003,12 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             // the per-lane tile line reject: lanes whose segment line is too far from the tile's axis
             // line leave the tile; a tile no lane keeps is skipped before it is staged
             const float4 *tq = reinterpret_cast<const float4 *>(tax + (int64_t)(~c));
-            const float4 ta = tq[0], tb = tq[1], tc = tq[2];
+            const float4 ta = tq[0], tb = tq[1];
             if (tb.w < 0.f) return;
             ScanStaged A;
             A.bu = mk(ta.x, ta.y, ta.z);
             A.m0 = mk(tb.x, tb.y, tb.z);
-            // the packet-local threshold: the packet box grown by the tile's region growth, projected
-            // onto the axis (s = x . d - pd), bounds the axis parameter of every contributing pB
-            float thr_t = ta.w;
-            if (tc.z < FLT_MAX) {
-                const float ax = ta.x * pbox_lo.x, bx = ta.x * pbox_hi.x;
-                const float ay = ta.y * pbox_lo.y, by = ta.y * pbox_hi.y;
-                const float az = ta.z * pbox_lo.z, bz = ta.z * pbox_hi.z;
-                const float slo = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz) - tc.w - tb.w;
-                const float shi = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz) - tc.w + tb.w;
-                const float ds = fmaxf(fabsf(slo - tc.x), fabsf(shi - tc.x)) * 1.0001f;
-                thr_t = fminf(thr_t, __builtin_fmaf(tc.z, ds, tc.y));
-            }
-            const float thr = thr_t + al_max;
+            const float thr = ta.w + al_max;
             A.thr_sq = thr < FLT_MAX ? thr * thr : INFINITY;
             A.uc = 1.0001f;
             onm &= scan_keep_mask(SL, L.au, A);
@@ -1607,7 +1546,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         hipLaunchKernelGGL(k_segbox, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
                            a.segbox);
         hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.bset, a.nvalid,
-                           a.leaf_size, a.segbox, a.R, a.tile_local, a.tileax);
+                           a.leaf_size, a.segbox, a.R, a.tileax);
         tax = a.tileax;
     }
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));

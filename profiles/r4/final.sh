@@ -5,11 +5,13 @@
 # leg, C3 and C4 at N=1.
 set -o pipefail
 OUT=${1:-gpurun_out/r4/final}
+PART=${2:-all}   # tests | bench | all (one gpurun call each for tests and bench keeps both inside 1200 s)
 mkdir -p "$OUT"
 ( while sleep 60; do echo "tick $(date +%T)"; done ) &
 TICK=$!
 trap 'kill $TICK' EXIT
 export TMPDIR=/tmp
+if [ "$PART" != bench ]; then
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 \
     || { tail -n 30 "$OUT/smoke.log"; exit 1; }
 tail -n 1 "$OUT/smoke.log"
@@ -17,6 +19,8 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 1100 --timeo
     > "$OUT/pytest_gpu.log" 2>&1 || { tail -n 40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -n 1 "$OUT/pytest_gpu.log"
 grep -E "^C[345]" "$OUT/pytest_gpu.log" | head -12
+fi
+[ "$PART" = tests ] && exit 0
 timeout -k 10 600 python -u bench.py --json-out "$OUT/bench.json" > "$OUT/bench.log" 2>&1 \
     || { tail -n 30 "$OUT/bench.log"; exit 1; }
 tail -n 1 "$OUT/bench.log" | cut -c1-600

@@ -1,13 +1,12 @@
 """The tile kernel's prefilter variants give the SAME per-segment results, bit for bit.
 
 Option 111 (prefilter margins: 1 = the round-3 rounding analysis, default; 0 = round 2's wider
-margins) and option 112 (the per-lane tile line reject: 1 = on with the packet-local threshold,
-default since round 4; 2 = on with the region-wide threshold only; 0 = off) only
+margins) and option 112 (the per-lane tile line reject: 1 = on, default since round 4; 0 = off) only
 change which NON-contributing (lane, beam) pairs reach the exact stage: a pair either margin rejects
 has every reference-computed distance >= R + r (tests/test_margin_bound.py), and a lane the tile line
 reject takes off a tile has no pair in it that can contribute (bre_gather.hip, above k_tile_axis).  Removing non-contributing pairs
 from the beam-major queue leaves the contributing pairs in the same relative order, so every
-per-segment sum and contribution count must be identical in all four combinations -- on real C2
+per-segment sum and contribution count must be identical in all combinations -- on real C2
 data (the production configuration: kernel 0, counters off, segment sort on) at a large and a small
 radius."""
 import numpy as np
@@ -28,7 +27,7 @@ def test_prefilter_options_are_bit_identical(bre, scene_mod_gpu, medium, iterati
     R = bre.beam_radius_at(0.01, 0.5, iteration)
     out = {}
     for margin in (1, 0):
-        for axis in (0, 1, 2):
+        for axis in (0, 1):
             with bre.BeamGather(0) as g:
                 g.set_option(111, margin)
                 g.set_option(112, axis)
