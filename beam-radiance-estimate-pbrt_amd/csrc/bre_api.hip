@@ -73,6 +73,7 @@ struct bre_ctx {
     int shard_block = 1;                  // tiles per side of the blocks dealt to the shards
     int shard_mode = 0;                   // BRE_OPT_SHARD_MODE: 0 image tiles, 1 packet ranges
     int roots_split = -1;  // split the roots buffer was computed for (-1: stale)
+    bool nodes4_ok = false;  // nodes4 holds the 4-wide view of the current tree
     int leaf2 = 64;          // kernel 0: beams per leaf tile of the tile tree (64 best at C2)
     int beam_key = 2;        // internal: tree order of the build (BuildBuffers::beam_key): 2 / 1 (start, end) Hilbert / Morton, 0 centroid
     int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
@@ -98,7 +99,7 @@ struct bre_ctx {
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem chk_x, chk_aux, chk_y;  // bre_device_check staging
-    DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox;
+    DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox, nodes4;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
@@ -151,6 +152,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->bset = BeamSet{};
     c->nnodes = 0;
     c->roots_split = -1;
+    c->nodes4_ok = false;
     c->stats = bre_stats{};
     c->stats.n_beams = n;
     if (n == 0) return BRE_OK;
@@ -475,6 +477,13 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
         c->roots_split = c->split;
     }
+    if (!c->nodes4_ok) {
+        // the tile kernel's 4-wide view of the tree (Node4), once per build
+        HIPCHK(c, c->nodes4.ensure(sizeof(Node4) * (size_t)c->nnodes));
+        HIPCHK(c, launch_collapse4(c->nodes.as<Node>(), c->nnodes, c->nodes4.as<Node4>(), c->stream));
+        c->nodes4_ok = true;
+    }
+    a.nodes4 = c->nodes4.as<Node4>();
     a.roots = c->roots.as<int32_t>();
     a.partial = c->partial.as<float>();
     HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)((chunk + 63) / 64 * 64)));  // whole packets
@@ -581,7 +590,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
-                     &c->tileax, &c->segbox,
+                     &c->tileax, &c->segbox, &c->nodes4,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,

@@ -43,6 +43,17 @@ struct alignas(16) Node {
 static_assert(sizeof(Node) == 64, "Node must be one 64-B line");
 
 constexpr int32_t kEmptyChild = INT32_MIN;
+
+// The tile kernel's 4-wide view of the binary tree (k_collapse4): record i holds the boxes and
+// indices of binary node i's grandchildren, in left-to-right order (a leaf child stands for itself,
+// empty slots are kEmptyChild), so one node visit tests two levels of the tree.  Boxes are SoA
+// (lo[axis][slot]) so a visit reads the record with two 64-B scalar loads.
+struct alignas(16) Node4 {
+    float lo[3][4], hi[3][4];
+    int32_t child[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4 must be two 64-B lines");
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
 constexpr int kMaxSplit = 256;         // max work roots (subtrees) per gather
@@ -162,6 +173,7 @@ struct GatherArgs {
     const float4 *pow;
     BeamSet bset;
     const Node *nodes;
+    const Node4 *nodes4 = nullptr;  // tile kernel: the 4-wide view of `nodes` (null: binary traversal)
     int64_t nvalid;
     int leaf_size;
     DevCounters *ctr;
@@ -274,6 +286,7 @@ hipError_t launch_device_check(int kind, int64_t n, const float *x, int n_aux, c
 
 // gather kernels (bre_gather.hip)
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);
+hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipStream_t s);
 hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStream_t s);
 hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s);
 

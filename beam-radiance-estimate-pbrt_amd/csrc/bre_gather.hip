@@ -47,6 +47,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
 #endif
+// BRE_TREE4 1 (default): the tile kernel walks the 4-wide view of its tree (Node4, k_collapse4);
+// 0: the binary walk, near child first (timing A/B)
+#ifndef BRE_TREE4
+#define BRE_TREE4 1
+#endif
 // BRE_RMW_ROUNDS: exact-stage read-modify-write rounds per batch, 64 (default) = every rank in
 // rounds (queue order, documented operations only); < 64 (timing A/B only) adds the ranks beyond
 // by LDS float atomics, whose same-address order within one instruction is not documented
@@ -886,9 +891,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int64_t nseg, const float *__restrict__ so, const float *__restrict__ sp_, const float *__restrict__ sd,
     const float *__restrict__ stmax, const SegRec *__restrict__ srec, float R, float *__restrict__ partial,
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, BeamSet bset,
-    const Node *__restrict__ nodes, int64_t nvalid, int leaf_size, const int32_t *__restrict__ roots, int S,
-    DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan, int margin,
-    const TileAxis *__restrict__ tax) {
+    const Node *__restrict__ nodes, const Node4 *__restrict__ nodes4, int64_t nvalid, int leaf_size,
+    const int32_t *__restrict__ roots, int S, DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan,
+    int margin, const TileAxis *__restrict__ tax) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
     // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
@@ -1122,6 +1127,87 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     };
 
     if (__ballot(valid) != 0ull) {
+#if BRE_TREE4
+        // Fixed-order walk of the 4-wide view (Node4): a visit tests the four grandchild boxes of a
+        // binary node; the leaf tiles it finds are scanned, in slot order, before the walk goes on
+        // with the lowest-slot internal child, the others stacked.  (The gather has no early exit, so
+        // any order finds every pair; a fixed one keeps the queue order a function of the tree.)
+        const int32_t root = roots[sub];
+        int32_t pc0 = 0, pc1 = 0, pc2 = 0, pc3 = 0;  // pending leaf tiles, in slot order
+        unsigned long long pm0 = 0ull, pm1 = 0ull, pm2 = 0ull, pm3 = 0ull;  // lanes on each one's box
+        int npend = 0;
+        int node = root;
+        bool have_node = root >= 0;
+        if (!have_node) {
+            pc0 = root;
+            pm0 = __ballot(valid);
+            npend = 1;
+        }
+        int sp = 0;
+        while (true) {
+#pragma nounroll
+            for (; npend > 0; --npend) {
+                leaf(pc0, pm0);
+                pc0 = pc1;
+                pm0 = pm1;
+                pc1 = pc2;
+                pm1 = pm2;
+                pc2 = pc3;
+                pm2 = pm3;
+            }
+            if (!have_node) {
+                if (sp == 0) break;
+                --sp;
+                node = sh.stk[sp];
+            }
+            node = __builtin_amdgcn_readfirstlane(node);
+            if (COUNT) ++visits;
+            const Node4 *nq = nodes4 + node;
+            int32_t nxt = 0;
+            have_node = false;
+            bool ovf = false;
+            // slots high to low: a leaf goes to the FRONT of the pending list and an internal child
+            // becomes the next node (the one it replaces is stacked), so both end in slot order
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {
+                const int32_t ck = nq->child[k];
+                const Box6 bk{nq->lo[0][k], nq->lo[1][k], nq->lo[2][k], nq->hi[0][k], nq->hi[1][k], nq->hi[2][k]};
+                float te;
+                const bool h = valid & (ck != kEmptyChild) & node_test(bk, L.o, L.invs, L.tmax, te);
+                const unsigned long long m = __ballot(h);
+                if (m != 0ull) {
+                    if (ck < 0) {
+                        pc3 = pc2;
+                        pm3 = pm2;
+                        pc2 = pc1;
+                        pm2 = pm1;
+                        pc1 = pc0;
+                        pm1 = pm0;
+                        pc0 = ck;
+                        pm0 = m;
+                        ++npend;
+                    } else {
+                        if (have_node) {
+                            if (sp >= stack_cap) {
+                                ovf = true;
+                            } else {
+                                sh.stk[sp] = nxt;
+                                ++sp;
+                            }
+                        }
+                        nxt = ck;
+                        have_node = true;
+                    }
+                }
+            }
+            if (ovf) {
+                // never silent: the host turns the flag into BRE_ERR_STATE (bre_api.hip)
+                if (lane == 0) atomicOr(&ctr->flags, kFlagStack);
+                break;
+            }
+            node = nxt;
+        }
+#else
         const int32_t root = roots[sub];
         // the production instantiation re-reads the lane's o, tmax and 1/d from its SegRec at each
         // node visit instead of holding them in VGPRs through the leaf scans (register budget)
@@ -1226,6 +1312,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
                 have_node = false;
             }
         }
+#endif
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
@@ -1508,6 +1595,52 @@ __global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *_
 
 }  // namespace
 
+// The 4-wide view (Node4): one thread per binary node.  Slot order is the binary order (child 0's
+// children, then child 1's), so a fixed-order walk of the 4-wide view visits the leaves in the same
+// left-to-right order as a fixed-order binary walk.  A grandchild box lies inside its parent's box, so
+// testing it directly prunes at least as tightly as testing both levels.
+__global__ __launch_bounds__(256) void k_collapse4(const Node *__restrict__ nodes, int64_t nnodes,
+                                                   Node4 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nnodes) return;
+    const Node &n = nodes[i];
+    Node4 q;
+    int k = 0;
+    const auto put = [&](int32_t c, const float *lo, const float *hi) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            q.lo[a][k] = lo[a];
+            q.hi[a][k] = hi[a];
+        }
+        q.child[k] = c;
+        ++k;
+    };
+    for (int c = 0; c < 2; ++c) {
+        const int32_t ch = n.child[c];
+        if (ch == kEmptyChild) continue;
+        if (ch >= 0) {
+            const Node &m = nodes[ch];
+            for (int d = 0; d < 2; ++d)
+                if (m.child[d] != kEmptyChild) put(m.child[d], m.lo[d], m.hi[d]);
+        } else {
+            put(ch, n.lo[c], n.hi[c]);
+        }
+    }
+    for (; k < 4; ++k) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q.lo[a][k] = q.hi[a][k] = 0.f;
+        q.child[k] = kEmptyChild;
+    }
+    q.pad[0] = q.pad[1] = q.pad[2] = q.pad[3] = 0;
+    out[i] = q;
+}
+
+hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipStream_t s) {
+    if (nnodes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_collapse4, dim3((unsigned int)((nnodes + 255) / 256)), dim3(256), 0, s, nodes, nnodes, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s) {
     hipLaunchKernelGGL(k_roots, dim3(1), dim3(256), 0, s, nodes, S, roots);
     return hipGetLastError();
@@ -1537,6 +1670,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     int32_t *pcnt = (counters || a.seg_counts) ? a.pcnt : nullptr;
     if ((counters || a.seg_counts) && !pcnt) return hipErrorInvalidValue;
     if (!a.segrec || a.leaf_size > 64) return hipErrorInvalidValue;
+    if (BRE_TREE4 && !a.nodes4) return hipErrorInvalidValue;  // the 4-wide walk needs the collapsed view
     hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
     const TileAxis *tax = nullptr;
@@ -1552,7 +1686,8 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
-                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nvalid, a.leaf_size,     \
+                       a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nodes4, a.nvalid,        \
+                       a.leaf_size,                                                                        \
                        a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin, tax)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
