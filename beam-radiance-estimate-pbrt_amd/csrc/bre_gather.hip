@@ -713,7 +713,14 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     (void)sd;
     const int sa = sl << 2;
     const auto shf = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(v))); };
+#if BRE_EXACT_SHFL == 3
+    // 3: every segment value by ds_bpermute (no SegRec load at all)
+    (void)sr;
+    const float4 bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
+    const float4 s1 = make_float4(shf(L.p.x), shf(L.p.y), shf(L.p.z), shf(L.mag_a));
+#else
     const float4 s1 = sr[64], bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
+#endif
     const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
     const float4 s0 = make_float4(shf(L.o.x), shf(L.o.y), shf(L.o.z), shf(L.tmax));
     const float4 s3 = make_float4(shf(L.invs.x), shf(L.invs.y), shf(L.invs.z), 0.f);
@@ -846,7 +853,8 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     unsigned long long before = 0ull;
     if (contrib) before = atomicOr(&sh.rkm[sl], lane_bit);
     int rank = contrib ? __popcll(before) : 64;
-    if (BRE_RANK_MODE == 0 && __ballot(contrib && (before & ~(lane_bit - 1ull)) != 0ull) != 0ull) {
+    // (a lane's own bit is never in its returned mask: a set bit at or above it means a higher lane went first)
+    if (BRE_RANK_MODE == 0 && __ballot(contrib && (before >> lane) != 0ull) != 0ull) {
         __builtin_amdgcn_wave_barrier();
         rank = contrib ? lanes_below(sh.rkm[sl]) : 64;
     }
