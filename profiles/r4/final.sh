@@ -2,7 +2,7 @@
 # Round 4 measurement (via gpurun): smoke(), the whole GPU suite (C3, C4, C5 full-size parity included),
 # the default bench line (C2: CPU leg, the roofline's PMC passes and the counter blocks at iterations 0
 # and 15 included), the rocprofv3 kernel-trace / HBM passes of the same workload, the C-ABI boundary
-# leg, C3 and C4 at N=1.
+# leg, C3 and C4 at N=1, and the multi-rank bench flow rehearsed with 2 / 4 ranks on the one GPU (gloo).
 set -o pipefail
 OUT=${1:-gpurun_out/r4/final}
 PART=${2:-all}   # tests | bench | all (one gpurun call each for tests and bench keeps both inside 1200 s)
@@ -32,6 +32,7 @@ timeout -k 10 300 python -u bench.py --workload c3 --steps 1 --warmup 0 --no-cpu
     > "$OUT/c3.log" 2>&1 || { tail -n 20 "$OUT/c3.log"; exit 1; }
 timeout -k 10 600 python -u bench.py --workload c4 --steps 1 --warmup 0 --no-cpu --no-pmc --no-diag \
     --json-out "$OUT/c4.json" > "$OUT/c4.log" 2>&1 || { tail -n 20 "$OUT/c4.log"; exit 1; }
+EXPLORE_OUT=${OUT#gpurun_out/}/rehearse bash profiles/rehearse_n2.sh || exit 1
 for f in bench bench_boundary c3 c4; do
   python3 -c "import json;d=json.load(open('$OUT/$f.json'));print('$f', 'value', round(d['value']), 'ms/step', round(d['ms_per_step'],1))"
 done
