@@ -245,6 +245,16 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     c->nnodes = nnodes;
     c->built_leaf_size = K;
     c->stats.n_nodes = nnodes;
+    if (c->kernel == 0 || c->kernel == 4) {
+        // the tile kernel's work roots and 4-wide view, here on the build's stream: with two contexts
+        // pipelined they overlap the other context's gather instead of preceding this one's
+        HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
+        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
+        c->roots_split = c->split;
+        HIPCHK(c, c->nodes4.ensure(sizeof(Node4) * (size_t)nnodes));
+        HIPCHK(c, launch_collapse4(c->nodes.as<Node>(), nnodes, c->nodes4.as<Node4>(), c->stream));
+        c->nodes4_ok = true;
+    }
     return BRE_OK;
 }
 

@@ -395,12 +395,15 @@ __global__ void k_segbox_init(unsigned int *__restrict__ b) {
     if (threadIdx.x < 6) b[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
 }
 
-// box of the launch's finite segment end points (6 ordered uints: min xyz, max xyz)
+// box of the launch's finite segment end points (6 ordered uints: min xyz, max xyz).  Grid-stride
+// over a bounded grid, reduced per wave and then per block in LDS: one set of six atomics per block
+// (per-wave atomics on the same six words serialised at the L2: 0.64 ms at C2's 0.6M segments)
+constexpr int kSegboxBlocks = 512;
 __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__restrict__ o, const float *__restrict__ p,
                                                 unsigned int *__restrict__ b) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ unsigned int red[4][6];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
-    if (i < nseg) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * 256) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const float *q = (e ? p : o) + 3 * i;
@@ -422,12 +425,23 @@ __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__res
             mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], off));
         }
     }
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            atomicMin(&b[k], mn[k]);
-            atomicMax(&b[3 + k], mx[k]);
+            red[w][k] = mn[k];
+            red[w][3 + k] = mx[k];
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        unsigned int v = red[0][k];
+        for (int j = 1; j < 4; ++j) v = k < 3 ? min(v, red[j][k]) : max(v, red[j][k]);
+        if (k < 3)
+            atomicMin(&b[k], v);
+        else
+            atomicMax(&b[k], v);
     }
 }
 
@@ -1461,38 +1475,64 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
 // The leaves below a Karras node are a contiguous range (bre_build.hip), found by its leftmost and
 // rightmost descents.  The partial sums are added in this root order (k_reduce): deterministic.
 __global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    __shared__ int32_t cur[kMaxSplit], nxt[kMaxSplit], wt[kMaxSplit];
-    __shared__ int n_sh;
+    // One block, one frontier entry per thread (S <= kMaxSplit = 256 = blockDim).  Level by level, the
+    // frontier's internal nodes are replaced by their children while the expanded frontier (counted
+    // with two entries per internal node) stays within S; then the work roots are ordered by the
+    // number of leaf tiles below them, largest first, ties in frontier order (a stable sort).
+    __shared__ int32_t cur[kMaxSplit], wt[kMaxSplit], cnt[kMaxSplit];
+    __shared__ int n_sh, stop_sh;
     if (blockIdx.x != 0) return;
-    if (threadIdx.x == 0) {
-        int n = 1;
+    const int t = threadIdx.x;
+    if (t == 0) {
         cur[0] = 0;
-        while (true) {
-            int m = 0;
-            for (int i = 0; i < n; ++i) m += (cur[i] >= 0) ? 2 : 1;
-            if (m > S) break;
-            bool grew = false;
-            m = 0;
-            for (int i = 0; i < n; ++i) {
-                if (cur[i] >= 0) {
-                    const Node &nd = nodes[cur[i]];
-                    if (nd.child[0] != kEmptyChild) nxt[m++] = nd.child[0];
-                    if (nd.child[1] != kEmptyChild) nxt[m++] = nd.child[1];
-                    grew = true;
-                } else {
-                    nxt[m++] = cur[i];
-                }
-            }
-            if (!grew) break;
-            for (int i = 0; i < m; ++i) cur[i] = nxt[i];
-            n = m;
-        }
-        n_sh = n;
+        n_sh = 1;
     }
     __syncthreads();
+    while (true) {
+        const int n = n_sh;
+        int32_t me = 0, c0 = kEmptyChild, c1 = kEmptyChild;
+        int real = 0, want = 0;
+        if (t < n) {
+            me = cur[t];
+            if (me >= 0) {
+                const Node &nd = nodes[me];
+                c0 = nd.child[0];
+                c1 = nd.child[1];
+                real = (c0 != kEmptyChild) + (c1 != kEmptyChild);
+                want = 2;
+            } else {
+                real = want = 1;
+            }
+        }
+        if (t < kMaxSplit) cnt[t] = real | (want << 8) | ((t < n && me >= 0) ? 1 << 16 : 0);
+        __syncthreads();
+        int pos = 0, m = 0, grew = 0, total = 0;
+        for (int j = 0; j < n; ++j) {  // the same order for every thread: LDS broadcasts
+            const int v = cnt[j];
+            if (j < t) pos += v & 0xff;
+            total += v & 0xff;
+            m += (v >> 8) & 0xff;
+            grew |= v >> 16;
+        }
+        if (t == 0) stop_sh = (m > S || !grew) ? 1 : 0;
+        __syncthreads();
+        if (stop_sh) break;
+        if (t < n) {
+            if (me >= 0) {
+                if (c0 != kEmptyChild) cur[pos++] = c0;  // written after every thread read its entry
+                if (c1 != kEmptyChild) cur[pos] = c1;
+            }
+        }
+        __syncthreads();
+        if (t < n && me < 0) cur[pos] = me;
+        if (t == 0) n_sh = total;
+        __syncthreads();
+    }
     const int n = n_sh;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        int32_t lo = cur[i], hi = cur[i];
+    int32_t r = 0, w = 0;
+    if (t < n) {
+        r = cur[t];
+        int32_t lo = r, hi = r;
         while (lo >= 0) {
             const Node &nd = nodes[lo];
             lo = nd.child[0] != kEmptyChild ? nd.child[0] : nd.child[1];
@@ -1501,25 +1541,20 @@ __global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, i
             const Node &nd = nodes[hi];
             hi = nd.child[1] != kEmptyChild ? nd.child[1] : nd.child[0];
         }
-        wt[i] = (~hi) - (~lo) + 1;
+        w = (~hi) - (~lo) + 1;
+        wt[t] = w;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int i = 1; i < n; ++i) {  // stable insertion sort, weight descending
-            const int32_t r = cur[i], w = wt[i];
-            int j = i - 1;
-            while (j >= 0 && wt[j] < w) {
-                cur[j + 1] = cur[j];
-                wt[j + 1] = wt[j];
-                --j;
-            }
-            cur[j + 1] = r;
-            wt[j + 1] = w;
+    if (t < n) {
+        int rank = 0;  // weight descending, ties in frontier order
+        for (int j = 0; j < n; ++j) {
+            const int32_t v = wt[j];
+            rank += (v > w) | ((v == w) & (j < t));
         }
-        for (int i = 0; i < n; ++i) roots[i] = cur[i];
-        for (int i = n; i < S; ++i) roots[i] = kEmptyChild;
-        roots[S] = n;
+        roots[rank] = r;
     }
+    if (t >= n && t < S) roots[t] = kEmptyChild;
+    if (t == 0) roots[S] = n;
 }
 
 template <bool COUNT>
@@ -1685,7 +1720,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     if (a.tileax && a.segbox && a.prefilter && a.nvalid > 0) {
         const int64_t ntiles = (a.nvalid + a.leaf_size - 1) / a.leaf_size;
         hipLaunchKernelGGL(k_segbox_init, dim3(1), dim3(64), 0, s, a.segbox);
-        hipLaunchKernelGGL(k_segbox, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
+        hipLaunchKernelGGL(k_segbox, dim3((unsigned int)std::min<int64_t>(kSegboxBlocks, (a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
                            a.segbox);
         hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.bset, a.nvalid,
                            a.leaf_size, a.segbox, a.R, a.tileax);
