@@ -38,7 +38,7 @@ struct alignas(16) Node {
     float hi[2][3];
     int32_t child[2];
     int32_t parent;
-    int32_t pad;
+    int32_t nleaf;  // leaf tiles below this node (k_karras: its key range; the work-root split sizes by it)
 };
 static_assert(sizeof(Node) == 64, "Node must be one 64-B line");
 

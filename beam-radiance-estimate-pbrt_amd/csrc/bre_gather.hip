@@ -398,7 +398,7 @@ __global__ void k_segbox_init(unsigned int *__restrict__ b) {
 // box of the launch's finite segment end points (6 ordered uints: min xyz, max xyz).  Grid-stride
 // over a bounded grid, reduced per wave and then per block in LDS: one set of six atomics per block
 // (per-wave atomics on the same six words serialised at the L2: 0.64 ms at C2's 0.6M segments)
-constexpr int kSegboxBlocks = 512;
+constexpr int kSegboxBlocks = 256;
 __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__restrict__ o, const float *__restrict__ p,
                                                 unsigned int *__restrict__ b) {
     __shared__ unsigned int red[4][6];
@@ -1475,78 +1475,69 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
 // The leaves below a Karras node are a contiguous range (bre_build.hip), found by its leftmost and
 // rightmost descents.  The partial sums are added in this root order (k_reduce): deterministic.
 __global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    // One block, one frontier entry per thread (S <= kMaxSplit = 256 = blockDim).  Level by level, the
-    // frontier's internal nodes are replaced by their children while the expanded frontier (counted
-    // with two entries per internal node) stays within S; then the work roots are ordered by the
-    // number of leaf tiles below them, largest first, ties in frontier order (a stable sort).
-    __shared__ int32_t cur[kMaxSplit], wt[kMaxSplit], cnt[kMaxSplit];
+    // One block, one frontier entry per thread (S <= kMaxSplit = 256 = blockDim).  Starting from the
+    // root, the frontier's LARGEST internal node (leaf tiles below it, Node::nleaf; ties: the lowest
+    // frontier position) is replaced by its children while the frontier stays within S entries, so
+    // the S work roots are as equal in size as the tree allows: the longest (packet, subtree) waves,
+    // which end the launch, are as short as they can be (a breadth-first frontier left subtrees of
+    // very unequal size, and an emulated 1/8 rank's iteration-0 gather 37% above 1/8 of N = 1's).
+    // Then the roots are ordered largest first (ties in frontier order) for the LPT block map.
+    __shared__ int32_t cur[kMaxSplit], wt[kMaxSplit];
+    __shared__ unsigned long long red[4];
     __shared__ int n_sh, stop_sh;
     if (blockIdx.x != 0) return;
     const int t = threadIdx.x;
+    const auto leaves = [&](int32_t c) -> int32_t { return c >= 0 ? nodes[c].nleaf : 1; };
     if (t == 0) {
         cur[0] = 0;
+        wt[0] = leaves(0);
         n_sh = 1;
     }
     __syncthreads();
     while (true) {
         const int n = n_sh;
-        int32_t me = 0, c0 = kEmptyChild, c1 = kEmptyChild;
-        int real = 0, want = 0;
-        if (t < n) {
-            me = cur[t];
-            if (me >= 0) {
-                const Node &nd = nodes[me];
-                c0 = nd.child[0];
-                c1 = nd.child[1];
-                real = (c0 != kEmptyChild) + (c1 != kEmptyChild);
-                want = 2;
-            } else {
-                real = want = 1;
-            }
+        // the largest internal entry: key = (leaves << 32) | ~position, maximised over the block
+        unsigned long long key = 0ull;
+        if (t < n && cur[t] >= 0) key = ((unsigned long long)(unsigned int)wt[t] << 32) | (0xffffffffu - (unsigned int)t);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned int lo = (unsigned int)__shfl_xor((int)(unsigned int)key, off);
+            const unsigned int hi = (unsigned int)__shfl_xor((int)(unsigned int)(key >> 32), off);
+            const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+            key = o > key ? o : key;
         }
-        if (t < kMaxSplit) cnt[t] = real | (want << 8) | ((t < n && me >= 0) ? 1 << 16 : 0);
+        if ((t & 63) == 0) red[t >> 6] = key;
         __syncthreads();
-        int pos = 0, m = 0, grew = 0, total = 0;
-        for (int j = 0; j < n; ++j) {  // the same order for every thread: LDS broadcasts
-            const int v = cnt[j];
-            if (j < t) pos += v & 0xff;
-            total += v & 0xff;
-            m += (v >> 8) & 0xff;
-            grew |= v >> 16;
+        if (t == 0) {
+            unsigned long long k = red[0];
+            for (int j = 1; j < 4; ++j) k = red[j] > k ? red[j] : k;
+            int stop = 1;
+            if (k != 0ull) {
+                const int i = (int)(0xffffffffu - (unsigned int)k);
+                const Node &nd = nodes[cur[i]];
+                const int32_t c0 = nd.child[0], c1 = nd.child[1];
+                const int add = (c0 != kEmptyChild) + (c1 != kEmptyChild) - 1;
+                if (n + add <= S) {
+                    stop = 0;
+                    const int32_t first = c0 != kEmptyChild ? c0 : c1;
+                    cur[i] = first;
+                    wt[i] = leaves(first);
+                    if (add == 1) {
+                        cur[n] = c1;
+                        wt[n] = leaves(c1);
+                    }
+                    n_sh = n + add;
+                }
+            }
+            stop_sh = stop;
         }
-        if (t == 0) stop_sh = (m > S || !grew) ? 1 : 0;
         __syncthreads();
         if (stop_sh) break;
-        if (t < n) {
-            if (me >= 0) {
-                if (c0 != kEmptyChild) cur[pos++] = c0;  // written after every thread read its entry
-                if (c1 != kEmptyChild) cur[pos] = c1;
-            }
-        }
-        __syncthreads();
-        if (t < n && me < 0) cur[pos] = me;
-        if (t == 0) n_sh = total;
-        __syncthreads();
     }
     const int n = n_sh;
-    int32_t r = 0, w = 0;
+    const int32_t r = t < n ? cur[t] : 0, w = t < n ? wt[t] : 0;
     if (t < n) {
-        r = cur[t];
-        int32_t lo = r, hi = r;
-        while (lo >= 0) {
-            const Node &nd = nodes[lo];
-            lo = nd.child[0] != kEmptyChild ? nd.child[0] : nd.child[1];
-        }
-        while (hi >= 0) {
-            const Node &nd = nodes[hi];
-            hi = nd.child[1] != kEmptyChild ? nd.child[1] : nd.child[0];
-        }
-        w = (~hi) - (~lo) + 1;
-        wt[t] = w;
-    }
-    __syncthreads();
-    if (t < n) {
-        int rank = 0;  // weight descending, ties in frontier order
+        int rank = 0;  // leaves descending, ties in frontier order
         for (int j = 0; j < n; ++j) {
             const int32_t v = wt[j];
             rank += (v > w) | ((v == w) & (j < t));
