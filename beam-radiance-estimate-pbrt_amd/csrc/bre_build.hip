@@ -54,6 +54,12 @@ __device__ __forceinline__ bool finite6(const float *b) {
 
 constexpr int kBlock = 256;
 
+__global__ void k_prep_init(unsigned int *__restrict__ cbounds, unsigned int *__restrict__ nvalid) {
+    const int t = threadIdx.x;
+    if (t < 12) cbounds[t] = ((t / 3) & 1) ? 0u : 0xffffffffu;  // min, max, min, max
+    if (t < 3) nvalid[t] = t == 1 ? 0xffffffffu : 0u;
+}
+
 // Grid-stride: each thread prepares several beams and keeps running centroid bounds; the block
 // reduces them (wave shuffles, then LDS across its 4 waves) and issues one set of atomics, so the
 // 7 contended global atomics are paid per block, not per wave (~3 ms -> ~0.2 ms at 2.7M beams).
@@ -381,7 +387,7 @@ __global__ __launch_bounds__(kBlock) void k_karras(const unsigned long long *__r
     }
     nodes[i].child[0] = left;
     nodes[i].child[1] = right;
-    nodes[i].pad = 0;
+    nodes[i].nleaf = hi - lo + 1;
     if (i == 0) nodes[0].parent = -1;
 }
 
@@ -454,7 +460,7 @@ __global__ void k_single(const BeamRec *__restrict__ recs, int64_t nvalid, int l
     n.child[0] = ~0;
     n.child[1] = kEmptyChild;
     n.parent = -1;
-    n.pad = 0;
+    n.nleaf = 1;
     nodes[0] = n;
 }
 
@@ -464,22 +470,15 @@ inline unsigned int grid_for(int64_t n) { return (unsigned int)((n + kBlock - 1)
 
 hipError_t launch_prep(const BuildBuffers &b, hipStream_t s) {
     // cbounds: centroid min = 0xffffffff, max = 0, then end-point min / max; nvalid = 0
-    hipError_t e = hipMemsetAsync(b.cbounds, 0xff, 3 * sizeof(unsigned int), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.cbounds + 3, 0, 3 * sizeof(unsigned int), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.cbounds + 6, 0xff, 3 * sizeof(unsigned int), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.cbounds + 9, 0, 3 * sizeof(unsigned int), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.nvalid, 0, sizeof(unsigned int), s);  // valid count
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.nvalid + 1, 0xff, sizeof(unsigned int), s);  // radius bits min
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.nvalid + 2, 0, sizeof(unsigned int), s);  // radius bits max
+    // the reduction targets' identities, one launch: centroid min / max, end-point min / max, then the
+    // valid count and the radius bits' min / max
+    hipLaunchKernelGGL(k_prep_init, dim3(1), dim3(64), 0, s, b.cbounds, b.nvalid);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (b.n == 0) return hipSuccess;
-    const unsigned prep_grid = (unsigned)std::min<int64_t>((int64_t)grid_for(b.n), 2048);  // grid-stride
+    // grid-stride over 512 blocks: each block's reduction ends in 14 same-address atomics, which the L2
+    // serialises (~70 ns each): 2048 blocks cost ~0.2 ms of them at C2
+    const unsigned prep_grid = (unsigned)std::min<int64_t>((int64_t)grid_for(b.n), 512);
     hipLaunchKernelGGL(k_prep, dim3(prep_grid), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.n, b.sqrt_mode,
                        b.box, b.cent, b.cbounds, b.nvalid);
     return hipGetLastError();

@@ -352,7 +352,8 @@ size_t seg_sort_temp_bytes(int64_t n) {
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     if (s.n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sort_init, dim3(1), dim3(64), 0, st, s.bounds);
-    const unsigned bgrid = grid_of(s.n) < 1024u ? grid_of(s.n) : 1024u;  // grid-stride bounds
+    // grid-stride bounds over at most 256 blocks (one set of six same-address atomics per block)
+    const unsigned bgrid = grid_of(s.n) < 256u ? grid_of(s.n) : 256u;
     hipLaunchKernelGGL(k_origin_bounds, dim3(bgrid), dim3(kBlock), 0, st, s.n, s.o, s.bounds);
     int key_bits = 50;
     if (s.key_mode == 1 || s.key_mode == 4) {
