@@ -102,6 +102,8 @@ struct bre_ctx {
     DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox, nodes4;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
+    DevMem ph_s_start, ph_s_end, ph_s_radius, ph_s_power;  // single-trace photon pass: per-photon beam slots
+    int photon_single = 1;  // internal (option 116): 1 single-trace photon pass (default), 0 two traces, 2..16 forced slots
     // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
     DevMem sc_tris, sc_nodes, sc_prims, sc_light_tri, sc_light_func, sc_light_cdf;
     uint64_t sc_hash = 0;  // hash of the uploaded triangles (0: none)
@@ -601,7 +603,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
                      &c->tileax, &c->segbox, &c->nodes4,
-                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->grid_dens, &c->cam_dev, &c->cam_perms,
+                     &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->ph_s_start, &c->ph_s_end, &c->ph_s_radius, &c->ph_s_power, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
                      &c->seg_depth, &c->ch_bounds, &c->ch_counts,
@@ -719,6 +721,11 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 114:  // internal: film accumulation, 1 deterministic per-pixel compose (default) / 0 float atomics (A/B)
         if (value != 0 && value != 1) return fail(c, BRE_ERR_INVALID_ARG, "film mode must be 0 or 1");
         c->film_compose = (int)value;
+        return BRE_OK;
+    case 116:  // internal: photon pass, 1 single trace with per-photon slots (default) / 0 two traces (A/B) /
+               // 2..16 single trace with that many slots per photon (tests: forces the overflow re-trace)
+        if (value < 0 || value > 16) return fail(c, BRE_ERR_INVALID_ARG, "photon pass mode must be in 0..16");
+        c->photon_single = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
@@ -928,8 +935,24 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     const DevScene *ds = c->ph_scene.as<DevScene>();
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     const int sdepth = c->sc_head.stack_depth;
-    HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(), nullptr,
-                             nullptr, nullptr, nullptr, nullptr, false, c->stream));
+    // single-trace form (bre_photon.hip): `cap` beam slots per photon, scratch near 1 GB (16 slots at 1M
+    // photons); below 4 slots, or with option 116 = 0, the two-trace form
+    int cap = c->photon_single ? (int)std::min<int64_t>(16, ((int64_t)1 << 30) / (40 * std::max<int64_t>(n_photons, 1))) : 0;
+    if (cap < 4) cap = 0;
+    if (c->photon_single >= 2) cap = c->photon_single;  // tests: a forced slot count (overflow paths)
+    if (cap > 0) {
+        const size_t slots = N * (size_t)cap;
+        HIPCHK(c, c->ph_s_start.ensure(slots * 3 * sizeof(float)));
+        HIPCHK(c, c->ph_s_end.ensure(slots * 3 * sizeof(float)));
+        HIPCHK(c, c->ph_s_radius.ensure(slots * sizeof(float)));
+        HIPCHK(c, c->ph_s_power.ensure(slots * 3 * sizeof(float)));
+        HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
+                                 nullptr, c->ph_s_start.as<float>(), c->ph_s_end.as<float>(), c->ph_s_radius.as<float>(),
+                                 c->ph_s_power.as<float>(), 2, cap, c->stream));
+    } else {
+        HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
+                                 nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, c->stream));
+    }
     HIPCHK(c, launch_count_scan(c->ph_tmp.ptr, c->ph_tmp.cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
                                 n_photons, c->stream));
     int64_t total = 0;
@@ -942,9 +965,15 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
         HIPCHK(c, c->in_end.ensure(B * 3 * sizeof(float)));
         HIPCHK(c, c->in_radius.ensure(B * sizeof(float)));
         HIPCHK(c, c->in_power.ensure(B * 3 * sizeof(float)));
+        if (cap > 0)
+            HIPCHK(c, launch_photon_slots(n_photons, cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
+                                          c->ph_s_start.as<float>(), c->ph_s_end.as<float>(), c->ph_s_radius.as<float>(),
+                                          c->ph_s_power.as<float>(), c->in_start.as<float>(), c->in_end.as<float>(),
+                                          c->in_radius.as<float>(), c->in_power.as<float>(), c->stream));
+        // every photon (two-trace form), or only those with more beams than slots
         HIPCHK(c, launch_photons(ds, sdepth, n_photons, seq0, max_depth, beam_radius, c->ph_counts.as<int32_t>(),
                                  c->ph_offsets.as<int64_t>(), c->in_start.as<float>(), c->in_end.as<float>(),
-                                 c->in_radius.as<float>(), c->in_power.as<float>(), true, c->stream));
+                                 c->in_radius.as<float>(), c->in_power.as<float>(), 1, cap, c->stream));
     }
     float photon_ms = 0.f;
     if (c->timing) {

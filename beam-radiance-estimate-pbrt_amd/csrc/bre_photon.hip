@@ -9,10 +9,13 @@
 // photon's own PCG32 sequence iter*N + i + 1 (:386-389), so each photon's beams, their order and
 // their bits are those of the reference's single-threaded loop.
 //
-// Output is deterministic and photon-major: pass 1 counts each photon's beams, an inclusive scan
-// gives offsets, pass 2 re-traces and writes beam k of photon i at offsets[i] + k.  Tracing twice
-// costs less than the atomics + sort a single pass would need to restore the order, and keeps
-// memory at exactly the beam count (the per-photon bound 2^maxdepth - 1 would be 31x at depth 5).
+// Output is deterministic and photon-major: beam k of photon i lands at offsets[i] + k, offsets the
+// inclusive scan of the per-photon counts.  The default single-trace form (round 4) traces each photon
+// once, writing its first `cap` beams to the photon's own slots of a scratch array and its count;
+// after the scan a copy puts the slots at their offsets, and only the photons with more than `cap`
+// beams are traced again, straight to their offsets (the same code and random sequence: the same
+// bits).  cap is sized so the scratch stays near 1 GB (16 slots at 1M photons; C2's photons average
+// 2.7 beams); the two-trace form (count, scan, re-trace every photon) is the fallback.
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_scan.hpp>
@@ -126,18 +129,22 @@ struct Frame {
     float beta[3];
 };
 
-template <bool EMIT>
+// MODE 0: count each photon's beams; 1: write them at offsets[i] + k (with over > 0: only the photons
+// whose count exceeds `over`, the single-trace form's overflow); 2: write the first `over` beams to
+// the photon's slots i * over + k and count them all.
+template <int MODE>
 __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__restrict__ Sp, int64_t n, uint64_t seq0,
                                                           int max_depth, float radius, int32_t *__restrict__ counts,
                                                           const int64_t *__restrict__ offsets, float *__restrict__ bs,
                                                           float *__restrict__ be, float *__restrict__ br,
-                                                          float *__restrict__ bp) {
+                                                          float *__restrict__ bp, int over) {
     const int64_t i = (int64_t)blockIdx.x * kPhotonBlock + threadIdx.x;
     if (i >= n) return;
+    if (MODE == 1 && over > 0 && counts[i] <= over) return;
     const DevScene &S = *Sp;
     Pcg rng;
     pcg_seed(rng, seq0 + (uint64_t)i);
-    int64_t w = EMIT ? offsets[i] : 0;
+    const int64_t w = MODE == 1 ? offsets[i] : (MODE == 2 ? i * (int64_t)over : 0);
     int cnt = 0;
 
     // ---- emission, photonbeam.cpp:393-418: a light by power, DiffuseAreaLight::Sample_Le ----
@@ -217,7 +224,7 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
             // beam for the whole surface-hit segment, powerEnd = Tr * beta (:289-294)
             float bm[3] = {1.f, 1.f, 1.f};
             if (S.medium) medium_tr_any(S, rng, o, d, tmax, bm);
-            if (EMIT) {
+            if (MODE == 1 || (MODE == 2 && cnt < over)) {
                 const int64_t k = w + cnt;
                 bs[3 * k + 0] = o.x;
                 bs[3 * k + 1] = o.y;
@@ -282,7 +289,30 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
         for (int c = 0; c < 3; ++c) beta[c] = f.beta[c];
         resume = true;
     }
-    if (!EMIT) counts[i] = cnt;
+    if (MODE != 1) counts[i] = cnt;
+}
+
+// The single-trace form's copy: photon i's first min(count, cap) beams from its slots to its offsets.
+__global__ __launch_bounds__(256) void k_photon_slots(int64_t n, int cap, const int32_t *__restrict__ counts,
+                                                      const int64_t *__restrict__ offsets, const float *__restrict__ ss,
+                                                      const float *__restrict__ se, const float *__restrict__ sr,
+                                                      const float *__restrict__ sp, float *__restrict__ bs,
+                                                      float *__restrict__ be, float *__restrict__ br,
+                                                      float *__restrict__ bp) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int m = min(counts[i], cap);
+    const int64_t w = offsets[i];
+    for (int k = 0; k < m; ++k) {
+        const int64_t a = i * (int64_t)cap + k, b = w + k;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            bs[3 * b + c] = ss[3 * a + c];
+            be[3 * b + c] = se[3 * a + c];
+            bp[3 * b + c] = sp[3 * a + c];
+        }
+        br[b] = sr[a];
+    }
 }
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kPhotonBlock - 1) / kPhotonBlock); }
@@ -291,15 +321,27 @@ inline unsigned grid_of(int64_t n) { return (unsigned)((n + kPhotonBlock - 1) / 
 
 hipError_t launch_photons(const DevScene *scene, int stack_depth, int64_t n, uint64_t seq0, int max_depth,
                           float radius, int32_t *counts, const int64_t *offsets, float *start, float *end,
-                          float *rad, float *power, bool emit, hipStream_t s) {
+                          float *rad, float *power, int mode, int over, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t lds = scene_stack_bytes(stack_depth, kPhotonBlock);
-    if (emit)
-        hipLaunchKernelGGL(k_photons<true>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
-                           radius, counts, offsets, start, end, rad, power);
+    if (mode == 1)
+        hipLaunchKernelGGL(k_photons<1>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
+                           radius, counts, offsets, start, end, rad, power, over);
+    else if (mode == 2)
+        hipLaunchKernelGGL(k_photons<2>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
+                           radius, counts, offsets, start, end, rad, power, over);
     else
-        hipLaunchKernelGGL(k_photons<false>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
-                           radius, counts, offsets, start, end, rad, power);
+        hipLaunchKernelGGL(k_photons<0>, dim3(grid_of(n)), dim3(kPhotonBlock), lds, s, scene, n, seq0, max_depth,
+                           radius, counts, offsets, start, end, rad, power, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_photon_slots(int64_t n, int cap, const int32_t *counts, const int64_t *offsets, const float *ss,
+                               const float *se, const float *sr, const float *sp, float *start, float *end,
+                               float *rad, float *power, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_photon_slots, dim3((unsigned int)((n + 255) / 256)), dim3(256), 0, s, n, cap, counts, offsets,
+                       ss, se, sr, sp, start, end, rad, power);
     return hipGetLastError();
 }
 

@@ -575,9 +575,15 @@ inline size_t scene_stack_bytes(int stack_depth, int block) {
 }
 
 // photon pass launchers (bre_photon.hip)
+// mode 0: count beams per photon; 1: write them at offsets (over > 0: only photons with more than `over`
+// beams); 2: write the first `over` beams to per-photon slots and count them all (single-trace form)
 hipError_t launch_photons(const DevScene *scene, int stack_depth, int64_t n, uint64_t seq0, int max_depth,
                           float radius, int32_t *counts, const int64_t *offsets, float *start, float *end,
-                          float *rad, float *power, bool emit, hipStream_t s);
+                          float *rad, float *power, int mode, int over, hipStream_t s);
+// the single-trace form's copy of each photon's slots to its offsets
+hipError_t launch_photon_slots(int64_t n, int cap, const int32_t *counts, const int64_t *offsets, const float *ss,
+                               const float *se, const float *sr, const float *sp, float *start, float *end,
+                               float *rad, float *power, hipStream_t s);
 size_t count_scan_temp_bytes(int64_t n);
 hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n,
                              hipStream_t s);

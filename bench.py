@@ -96,6 +96,7 @@ def parse(argv=None):
     ap.add_argument("--tile-axis", type=int, default=-1, help=argparse.SUPPRESS)  # tile line reject A/B (option 112)
     ap.add_argument("--split-records", type=int, default=-1, help=argparse.SUPPRESS)  # BeamRec layout A/B (option 113)
     ap.add_argument("--film-compose", type=int, default=-1, help=argparse.SUPPRESS)  # film accumulation A/B (option 114)
+    ap.add_argument("--photon-single", type=int, default=-1, help=argparse.SUPPRESS)  # photon pass form A/B (option 116)
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
@@ -345,7 +346,8 @@ def make_context(bre, args, dev):
         c.set_option(bre.OPT_CHUNK_LEAF, args.chunk_leaf)
     for opt, val in ((102, args.occupancy if args.occupancy else -1), (bre.OPT_TILE_LEAF, args.tile_leaf or -1),
                      (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
-                     (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose)):
+                     (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose),
+                     (116, args.photon_single)):
         if val >= 0:
             c.set_option(opt, val)
     st = torch.cuda.Stream(dev)
