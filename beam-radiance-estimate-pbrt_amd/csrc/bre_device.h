@@ -56,7 +56,7 @@ struct alignas(16) Node4 {
 static_assert(sizeof(Node4) == 128, "Node4 must be two 64-B lines");
 constexpr int kStackDepth = 128;     // wave-uniform traversal stack (entries per wave)
 constexpr int kThreadStackDepth = 64;  // per-thread stack of the thread-per-segment kernel
-constexpr int kMaxSplit = 256;         // max work roots (subtrees) per gather
+constexpr int kMaxSplit = 1024;         // max work roots (subtrees) per gather
 
 // DevCounters::flags bits.  The host reads the word at every synchronising call and turns a set bit
 // into an error (bre_api.hip: check_flags), whatever the counters option.

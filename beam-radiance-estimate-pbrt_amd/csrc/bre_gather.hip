@@ -1474,8 +1474,8 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
 // waves on the largest subtrees are dispatched first and the kernel's tail is made of small ones.
 // The leaves below a Karras node are a contiguous range (bre_build.hip), found by its leftmost and
 // rightmost descents.  The partial sums are added in this root order (k_reduce): deterministic.
-__global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    // One block, one frontier entry per thread (S <= kMaxSplit = 256 = blockDim).  Starting from the
+__global__ __launch_bounds__(kMaxSplit) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
+    // One block, one frontier entry per thread (S <= kMaxSplit = blockDim).  Starting from the
     // root, the frontier's LARGEST internal node (leaf tiles below it, Node::nleaf; ties: the lowest
     // frontier position) is replaced by its children while the frontier stays within S entries, so
     // the S work roots are as equal in size as the tree allows: the longest (packet, subtree) waves,
@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, i
     // very unequal size, and an emulated 1/8 rank's iteration-0 gather 37% above 1/8 of N = 1's).
     // Then the roots are ordered largest first (ties in frontier order) for the LPT block map.
     __shared__ int32_t cur[kMaxSplit], wt[kMaxSplit];
-    __shared__ unsigned long long red[4];
+    __shared__ unsigned long long red[kMaxSplit / 64];
     __shared__ int n_sh, stop_sh;
     if (blockIdx.x != 0) return;
     const int t = threadIdx.x;
@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(256) void k_roots(const Node *__restrict__ nodes, i
         __syncthreads();
         if (t == 0) {
             unsigned long long k = red[0];
-            for (int j = 1; j < 4; ++j) k = red[j] > k ? red[j] : k;
+            for (int j = 1; j < kMaxSplit / 64; ++j) k = red[j] > k ? red[j] : k;
             int stop = 1;
             if (k != 0ull) {
                 const int i = (int)(0xffffffffu - (unsigned int)k);
@@ -1676,7 +1676,7 @@ hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipSt
 }
 
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s) {
-    hipLaunchKernelGGL(k_roots, dim3(1), dim3(256), 0, s, nodes, S, roots);
+    hipLaunchKernelGGL(k_roots, dim3(1), dim3(kMaxSplit), 0, s, nodes, S, roots);
     return hipGetLastError();
 }
 

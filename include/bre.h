@@ -72,7 +72,7 @@ typedef enum bre_option {
                                 rejected.  Every kernel gives the same pair contributions. */
     BRE_OPT_LEAF_SIZE = 4,   /* beams per BVH leaf cluster, 1..64 (default 1); applies at next build */
     BRE_OPT_SQRT_MODE = 5,   /* 0 = libstdc++ reading of WorldBound's sqrt (double), 1 = float */
-    BRE_OPT_SPLIT = 6,       /* kernels 0/4: BVH subtrees per segment packet, power of two 1..256 (default 256) */
+    BRE_OPT_SPLIT = 6,       /* kernels 0/4: BVH subtrees per segment packet, power of two 1..1024 (default 256) */
     BRE_OPT_PREFILTER = 7,   /* kernels 0/4/5: 0/1 conservative line-distance rejects before the exact
                                 closest-point code (default 1; results are identical either way) */
     BRE_OPT_SHARD_RANK = 8,  /* camera pass: walk only the 16x16 pixel tiles (the reference's
