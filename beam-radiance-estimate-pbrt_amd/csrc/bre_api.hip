@@ -701,8 +701,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 1 || value > ((int64_t)1 << 20)) return fail(c, BRE_ERR_INVALID_ARG, "partial cap must be in 1..2^20 MiB");
         c->partial_cap = value << 20;
         return BRE_OK;
-    case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated / 3 LPT / 4 LPT, packets reversed
-        if (value < 0 || value > 4) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0..4");
+    case 107:  // internal: tile kernel block mapping, 0 XCD-aware subtrees / 1 rotated / 3 LPT (sweeps)
+        if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0..3");
         c->block_map = (int)value;
         return BRE_OK;
     case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)

@@ -924,12 +924,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     // L2 serves one eighth of the tree).  Speed only, never correctness.
     int sub;
     int64_t grp;
-    if (map == 3 || map == 4) {
-        // LPT: all packets on the largest subtree (roots are sorted by size), then the next, ...;
-        // map 4 takes each subtree's packets in reverse order (the deeper, bounce-segment packets first)
+    if (map == 3) {
+        // LPT: all packets on the largest subtree (roots are sorted by size), then the next, ...
         const unsigned P = gridDim.x / (unsigned)S;
         grp = blockIdx.x % P;
-        if (map == 4) grp = (int64_t)(P - 1u) - grp;
         sub = (int)(blockIdx.x / P);
     } else if (map == 1) {
         grp = blockIdx.x / (unsigned)S;
