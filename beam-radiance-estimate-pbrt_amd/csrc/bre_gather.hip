@@ -1111,16 +1111,26 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         if (transposed) {
             // lane j: beam j (Ab' = -inf staged for a beam the packet rejects), segment i on the tile
             unsigned long long rest = onm;
+            // two on-lane segments per step (independent readlanes and tests: ILP), queued in order
             while (rest != 0ull) {
-                const int i = __ffsll((long long)rest) - 1;
+                const int i1 = __ffsll((long long)rest) - 1;
                 rest &= rest - 1ull;
-                ScanLane Si;
-                Si.q = mk(readlane_f(SL.q.x, i), readlane_f(SL.q.y, i), readlane_f(SL.q.z, i));
-                Si.al = 0.f;
-                const f3 aui = mk(readlane_f(L.au.x, i), readlane_f(L.au.y, i), readlane_f(L.au.z, i));
+                const bool two = rest != 0ull;
+                const int i2 = two ? __ffsll((long long)rest) - 1 : i1;
+                if (two) rest &= rest - 1ull;
+                ScanLane S1, S2;
+                S1.q = mk(readlane_f(SL.q.x, i1), readlane_f(SL.q.y, i1), readlane_f(SL.q.z, i1));
+                S2.q = mk(readlane_f(SL.q.x, i2), readlane_f(SL.q.y, i2), readlane_f(SL.q.z, i2));
+                S1.al = S2.al = 0.f;
+                const f3 au1 = mk(readlane_f(L.au.x, i1), readlane_f(L.au.y, i1), readlane_f(L.au.z, i1));
+                const f3 au2 = mk(readlane_f(L.au.x, i2), readlane_f(L.au.y, i2), readlane_f(L.au.z, i2));
                 // & km: a beam the packet rejected (thr_sq = -inf) still passes scan_keep_mask when it
                 // is near-parallel to segment i (u < 0.0101); the beam-major scan never visits it
-                push(scan_keep_mask(Si, aui, scan_beam_lds(sh.tile, lane)) & km, (int32_t)(cur_first + lane), i);
+                const ScanStaged Bl = scan_beam_lds(sh.tile, lane);
+                const unsigned long long n1 = scan_keep_mask(S1, au1, Bl) & km;
+                const unsigned long long n2 = scan_keep_mask(S2, au2, Bl) & km;
+                push(n1, (int32_t)(cur_first + lane), i1);
+                if (two) push(n2, (int32_t)(cur_first + lane), i2);
                 drain();
             }
             if (BRE_PHASE_TIMING) ph_scan += (phase_clock() - l1) - (ph_exact - ex0);
