@@ -929,6 +929,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         const unsigned P = gridDim.x / (unsigned)S;
         grp = blockIdx.x % P;
         sub = (int)(blockIdx.x / P);
+    } else if (map == 1) {
+        grp = blockIdx.x / (unsigned)S;
+        sub = (int)((blockIdx.x % (unsigned)S + grp) % (unsigned)S);
     } else if (map == 2 || S < 8) {
         sub = (int)(blockIdx.x % (unsigned)S);
         grp = blockIdx.x / (unsigned)S;
