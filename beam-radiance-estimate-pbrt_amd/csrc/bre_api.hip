@@ -103,7 +103,7 @@ struct bre_ctx {
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     DevMem ph_s_start, ph_s_end, ph_s_radius, ph_s_power;  // single-trace photon pass: per-photon beam slots
-    int photon_single = 1;  // internal (option 116): 1 single-trace photon pass (default), 0 two traces, 2..16 forced slots
+    int photon_single = 1;  // internal (option 116): 1 single-trace photon pass (default), 0 two traces, 2..64 forced slots
     // scene geometry on the device (upload_scene): triangles, BVHAccel nodes + primitive order, lights
     DevMem sc_tris, sc_nodes, sc_prims, sc_light_tri, sc_light_func, sc_light_cdf;
     uint64_t sc_hash = 0;  // hash of the uploaded triangles (0: none)
@@ -723,8 +723,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->film_compose = (int)value;
         return BRE_OK;
     case 116:  // internal: photon pass, 1 single trace with per-photon slots (default) / 0 two traces (A/B) /
-               // 2..16 single trace with that many slots per photon (tests: forces the overflow re-trace)
-        if (value < 0 || value > 16) return fail(c, BRE_ERR_INVALID_ARG, "photon pass mode must be in 0..16");
+               // 2..64 single trace with that many slots per photon (tests: forces the overflow re-trace)
+        if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "photon pass mode must be in 0..64");
         c->photon_single = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
@@ -935,9 +935,11 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     const DevScene *ds = c->ph_scene.as<DevScene>();
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     const int sdepth = c->sc_head.stack_depth;
-    // single-trace form (bre_photon.hip): `cap` beam slots per photon, scratch near 1 GB (16 slots at 1M
-    // photons); below 4 slots, or with option 116 = 0, the two-trace form
-    int cap = c->photon_single ? (int)std::min<int64_t>(16, ((int64_t)1 << 30) / (40 * std::max<int64_t>(n_photons, 1))) : 0;
+    // single-trace form (bre_photon.hip): `cap` beam slots per photon, scratch at most 2.5 GB (62 slots at
+    // 1M photons: the re-trace of the photons with more beams than slots is the form's tail, 1.65 ms
+    // with 16 slots vs 1.41 with 64 at C2, profiles/r4/run36); below 4 slots, or with option 116 = 0,
+    // the two-trace form
+    int cap = c->photon_single ? (int)std::min<int64_t>(64, ((int64_t)5 << 29) / (40 * std::max<int64_t>(n_photons, 1))) : 0;
     if (cap < 4) cap = 0;
     if (c->photon_single >= 2) cap = c->photon_single;  // tests: a forced slot count (overflow paths)
     if (cap > 0) {

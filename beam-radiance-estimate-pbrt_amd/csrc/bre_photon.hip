@@ -14,8 +14,9 @@
 // once, writing its first `cap` beams to the photon's own slots of a scratch array and its count;
 // after the scan a copy puts the slots at their offsets, and only the photons with more than `cap`
 // beams are traced again, straight to their offsets (the same code and random sequence: the same
-// bits).  cap is sized so the scratch stays near 1 GB (16 slots at 1M photons; C2's photons average
-// 2.7 beams); the two-trace form (count, scan, re-trace every photon) is the fallback.
+// bits).  cap is sized so the scratch stays within 2.5 GB (62 slots at 1M photons; C2's photons
+// average 2.7 beams, but the few long paths re-traced past 16 slots cost 0.25 ms); the two-trace form
+// (count, scan, re-trace every photon) is the fallback.
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_scan.hpp>

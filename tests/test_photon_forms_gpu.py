@@ -2,7 +2,7 @@
 offsets, and a re-trace of only the photons with more beams than slots) gives the SAME beam array,
 bit for bit and in the same order, as the two-trace form (count, scan, re-trace every photon) --
 bre_photon.hip, option 116.  Forced slot counts of 2 and 3 make many photons overflow, so the
-overflow re-trace is exercised; the default (16 slots at these photon counts) rarely overflows.
+overflow re-trace is exercised; the default (64 slots at these photon counts) rarely overflows.
 Both are checked against the recursive CPU restatement in tests/test_photon_gpu.py."""
 import numpy as np
 import pytest
