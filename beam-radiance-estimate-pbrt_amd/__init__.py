@@ -195,13 +195,15 @@ class BeamGather:
     def set_option(self, opt: int, value: int):
         self._check(self.lib.bre_set_option(self.h, opt, int(value)))
 
-    def set_shard(self, rank: int, count: int, block: int = 1, packets: bool = False):
+    def set_shard(self, rank: int, count: int, block: int = 1, packets: bool = False, roots: bool = False):
         """Tile shards (default): the camera pass walks only the 16x16 image tiles of the blocks of
         block x block tiles whose row-major block index is rank (mod count) (dist.tile_pixels lists the
         same pixels).  packets=True: the whole camera pass, and the gather of this rank's chunks of
         `block` consecutive sorted packets, chunk c to rank c mod count (shard_packet_index); the ranks'
-        films sum to the whole film."""
-        self.set_option(OPT_SHARD_MODE, 1 if packets else 0)
+        films sum to the whole film.  roots=True (BRE_OPT_SHARD_MODE 2): the whole camera pass, and the
+        gather of every segment against this rank's work roots (rank, rank + count, ... of the
+        size-ordered list); the ranks' films sum to the whole film."""
+        self.set_option(OPT_SHARD_MODE, 2 if roots else (1 if packets else 0))
         self.set_option(OPT_SHARD_BLOCK, int(block))
         self.set_option(OPT_SHARD_COUNT, int(count))
         self.set_option(OPT_SHARD_RANK, int(rank))

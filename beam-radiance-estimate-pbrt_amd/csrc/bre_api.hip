@@ -99,7 +99,7 @@ struct bre_ctx {
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem chk_x, chk_aux, chk_y;  // bre_device_check staging
-    DevMem counters_buf, roots, partial, pcnt, segrec, tileax, segbox, nodes4;
+    DevMem counters_buf, roots, roots_sh, partial, pcnt, segrec, tileax, segbox, nodes4;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     DevMem ph_s_start, ph_s_end, ph_s_radius, ph_s_power;  // single-trace photon pass: per-photon beam slots
@@ -476,7 +476,12 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     // and the grid within HIP's 2^32 work items.  Every segment's sum is still its subtrees'
     // partials added in root order by k_reduce: the per-segment results do not depend on the split.
     const bool want_cnt = c->counters || seg_counts;
-    const size_t per_seg = (size_t)c->split * (12 + (want_cnt ? 8 : 0));
+    // work-root shards (BRE_OPT_SHARD_MODE 2): this shard takes every count-th work root of the
+    // size-ordered list (rank, rank + count, ...) for ALL segments, so its waves sweep whole subtrees
+    // with every packet, as one GPU does; the per-segment sums are this shard's subtrees' share
+    const bool rshard = c->shard_mode == 2 && c->shard_count > 1;
+    const int S_eff = rshard ? (c->split + c->shard_count - 1) / c->shard_count : c->split;
+    const size_t per_seg = (size_t)S_eff * (12 + (want_cnt ? 8 : 0));
     int64_t chunk = c->partial_cap / (int64_t)per_seg / 64 * 64;
     // the exact stage addresses a launch's SegRec records with 32-bit byte offsets (BRE_BUF_LOADS):
     // at most 2^26 segments (64 B each) per launch
@@ -484,7 +489,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     if (chunk < 64) chunk = 64;
     if (chunk > nseg) chunk = nseg;
     HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
-    HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)chunk * (size_t)c->split));
+    HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)chunk * (size_t)S_eff));
     if (c->roots_split != c->split) {
         HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
         c->roots_split = c->split;
@@ -497,11 +502,18 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     }
     a.nodes4 = c->nodes4.as<Node4>();
     a.roots = c->roots.as<int32_t>();
+    if (rshard) {
+        HIPCHK(c, c->roots_sh.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
+        HIPCHK(c, launch_roots_shard(c->roots.as<int32_t>(), c->split, c->shard_rank, c->shard_count, S_eff,
+                                     c->roots_sh.as<int32_t>(), c->stream));
+        a.roots = c->roots_sh.as<int32_t>();
+        a.split = S_eff;
+    }
     a.partial = c->partial.as<float>();
     HIPCHK(c, c->segrec.ensure(sizeof(SegRec) * (size_t)((chunk + 63) / 64 * 64)));  // whole packets
     a.segrec = c->segrec.as<SegRec>();
     if (want_cnt) {
-        HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)chunk * (size_t)c->split));
+        HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)chunk * (size_t)S_eff));
         a.pcnt = c->pcnt.as<int32_t>();
     }
     if (c->tile_axis && a.leaf_size > 0) {
@@ -602,7 +614,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
-                     &c->tileax, &c->segbox, &c->nodes4,
+                     &c->tileax, &c->segbox, &c->nodes4, &c->roots_sh,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->ph_s_start, &c->ph_s_end, &c->ph_s_radius, &c->ph_s_power, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -672,7 +684,7 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         c->shard_block = (int)value;
         return BRE_OK;
     case BRE_OPT_SHARD_MODE:
-        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_MODE must be 0 or 1");
+        if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_MODE must be 0, 1 or 2");
         c->shard_mode = (int)value;
         return BRE_OK;
     case BRE_OPT_SHARD_COUNT:
@@ -1070,7 +1082,7 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
                             c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
                             c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count,
-                            c->shard_mode == 1 ? 0 : c->shard_block, c->stream));
+                            c->shard_mode != 0 ? 0 : c->shard_block, c->stream));
     // total = offs[S-1] + valid[S-1]
     HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
     int64_t last_off = 0;

@@ -287,6 +287,8 @@ hipError_t launch_device_check(int kind, int64_t n, const float *x, int n_aux, c
 // gather kernels (bre_gather.hip)
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);
 hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipStream_t s);
+hipError_t launch_roots_shard(const int32_t *roots, int S, int rank, int count, int S2, int32_t *out,
+                              hipStream_t s);
 hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStream_t s);
 hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s);
 

@@ -1685,6 +1685,22 @@ hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipSt
     return hipGetLastError();
 }
 
+// A work-root shard's list: the roots rank, rank + count, ... of the size-ordered list (so every shard
+// gets large and small subtrees), S2 entries padded with kEmptyChild, their number in out[S2].
+__global__ void k_roots_shard(const int32_t *__restrict__ roots, int S, int rank, int count, int S2,
+                              int32_t *__restrict__ out) {
+    const int n = roots[S];
+    const int n2 = n > rank ? (n - rank + count - 1) / count : 0;
+    for (int k = threadIdx.x; k < S2; k += blockDim.x) out[k] = k < n2 ? roots[rank + k * count] : kEmptyChild;
+    if (threadIdx.x == 0) out[S2] = n2;
+}
+
+hipError_t launch_roots_shard(const int32_t *roots, int S, int rank, int count, int S2, int32_t *out,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_roots_shard, dim3(1), dim3(256), 0, s, roots, S, rank, count, S2, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s) {
     hipLaunchKernelGGL(k_roots, dim3(1), dim3(kMaxSplit), 0, s, nodes, S, roots);
     return hipGetLastError();

@@ -100,7 +100,7 @@ def parse(argv=None):
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
-    ap.add_argument("--shard-mode", choices=["packets", "tiles"], default="packets",
+    ap.add_argument("--shard-mode", choices=["packets", "tiles", "roots"], default="packets",
                     help="strong scaling: each GPU gathers a range of the sorted segment packets (default) "
                          "or owns image tiles")
     ap.add_argument("--shard-block", type=int, default=1,
@@ -202,7 +202,7 @@ def main():
     if args.emulate_shard and world == 1:  # one rank's share of an N-GPU strong-scaling run, on this GPU
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
-                              packets=args.shard_mode == "packets")
+                              packets=args.shard_mode in ("packets", "roots"))
     def make_ctx():
         return make_context(bre, args, dev)
 
@@ -562,7 +562,7 @@ class SceneWorkload:
             self.scene = sc.cornell_scene(0.05, 0.5, preset["g"])
         self.W, self.H = frame.w, frame.h
         for c, _ in ctxs:
-            c.set_shard(shard_rank, shard_count, frame.block, frame.packets)
+            c.set_shard(shard_rank, shard_count, frame.block, frame.packets, roots=args.shard_mode == "roots")
         self.shard = (shard_rank, shard_count)
         self.ld = frame.accum
         # one iteration image per context (the camera pass's surface radiance, then the gather's
@@ -647,7 +647,10 @@ class SceneWorkload:
             film.add_(ld)
             self._last_add = torch.cuda.Event()
             self._last_add.record(st)
-        if self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
+        if self.args.shard_mode == "roots" and self.shard[1] > 1:  # every segment, 1/count of the subtrees
+            r, cnt = self.shard
+            n = n // cnt + (1 if r < n % cnt else 0)  # the ranks' shares sum to the estimates
+        elif self.frame.packets and self.shard[1] > 1:  # this rank gathers its range of the packets
             n = self.bre.shard_segments(n, *self.shard, self.frame.block)
         self.last_nseg = n
         return n
@@ -693,6 +696,7 @@ class SceneWorkload:
                f"GridDensityMedium smoke {a.grid_n}^3 (sigma_a 0.5, sigma_s 4.5, g 0.7)")
         film = (f"{a.width}x{a.height} per GPU" if a.scaling != "strong" else
                 f"{a.width}x{a.height}, the sorted segment packets split over the GPUs" if a.shard_mode == "packets"
+                else f"{a.width}x{a.height}, the BVH work roots split over the GPUs" if a.shard_mode == "roots"
                 else f"{a.width}x{a.height} split by 16x16 tiles over the GPUs")
         return {"workload": f"{self.name.upper()}: Cornell box + {med}, {a.photons / 1e6:g}M photons/iteration, "
                             f"{film}, maxdepth {a.max_depth}, R0 {a.radius}, alpha {a.alpha}",
@@ -702,6 +706,9 @@ class SceneWorkload:
                 "parallelism": (f"segment packets x{world} ({a.scaling} scaling), photons traced and camera pass "
                                 "on every rank, one RCCL reduce of the partial films per written image"
                                 if a.shard_mode == "packets" else
+                                f"BVH work roots x{world} ({a.scaling} scaling), photons traced and camera pass "
+                                "on every rank, one RCCL reduce of the partial films per written image"
+                                if a.shard_mode == "roots" else
                                 f"image tiles x{world} ({a.scaling} scaling), photons traced on every rank, "
                                 "one RCCL gather of the owned-pixel bands per written image"),
                 "kernel": KERNEL_NAMES.get(a.kernel, str(a.kernel)), "split": a.split,

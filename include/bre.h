@@ -97,7 +97,11 @@ typedef enum bre_option {
                                 by one shard.  1: PACKET shards -- every shard runs the whole camera
                                 pass and gathers its round-robin share of the sorted 64-segment packets
                                 (bre_shard_segments); the surface radiance of pixel p is added by shard
-                                p % count; the shards' Ld films SUM to the whole film (a reduce) */
+                                p % count; the shards' Ld films SUM to the whole film (a reduce).
+                                2: WORK-ROOT shards -- every shard runs the whole camera pass and
+                                gathers every segment against the BVH work roots rank, rank + count, ...
+                                of the size-ordered list (kernels 0/4); surface radiance and films as
+                                in 1, per-segment outputs are the shard's subtrees' partial sums */
 } bre_option;
 
 typedef struct bre_stats {
