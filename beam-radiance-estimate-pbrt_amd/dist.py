@@ -17,6 +17,10 @@ round-robin share of the sorted 64-segment packets (p = rank mod N, ``bre_shard_
 packets are exactly the single-GPU packets and every rank gets the same mix of cheap and costly ones (tile shards thin out each rank's bounce segments N-fold and loosen its
 packets: 1.5M vs 2.3M estimates/s per GPU at N=8, profiles/r2/explore/explore28-29).  A pixel's
 segments may then sit on several ranks: the films are partial sums, combined by one RCCL reduce.
+
+Work-root shards (bench ``--shard-mode roots``, BRE_OPT_SHARD_MODE 2; the frame is built with
+``packets=True``): every rank gathers every segment against its share of the BVH work roots, so its
+films are partial sums too and take the same reduce.
 """
 from __future__ import annotations
 
