@@ -27,6 +27,7 @@ STATUS_NAMES = {0: "BRE_OK", 1: "BRE_ERR_INVALID_ARG", 2: "BRE_ERR_HIP", 3: "BRE
 OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, OPT_PREFILTER = 1, 2, 3, 4, 5, 6, 7
 OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
 OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS, OPT_SHARD_BLOCK, OPT_SHARD_MODE = 11, 12, 13, 14, 15
+OPT_FILM_CLASSES, FILM_CLASSES = 16, 8
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -37,7 +38,7 @@ EXPORTS = [
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
     "bre_render_progressive", "bre_shard_segments", "bre_set_beams_sharded", "bre_gather_sharded",
-    "bre_device_check",
+    "bre_device_check", "bre_resolve_classes",
 ]
 
 
@@ -143,6 +144,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.bre_set_beams_sharded.restype = I32
     lib.bre_gather_sharded.argtypes = [P, I32, I64, P, P, P, P, P, F, I64, P, P, P]
     lib.bre_gather_sharded.restype = I32
+    if hasattr(lib, "bre_resolve_classes"):  # (absent from round-4 libraries loaded for A/B timing)
+        lib.bre_resolve_classes.argtypes = [P, I64, P, P]
+        lib.bre_resolve_classes.restype = I32
     if hasattr(lib, "bre_device_check"):  # (absent from round-3 libraries loaded for A/B timing)
         lib.bre_device_check.argtypes = [P, I32, I64, P, I32, P, P]
         lib.bre_device_check.restype = I32
@@ -207,6 +211,17 @@ class BeamGather:
         self.set_option(OPT_SHARD_BLOCK, int(block))
         self.set_option(OPT_SHARD_COUNT, int(count))
         self.set_option(OPT_SHARD_RANK, int(rank))
+
+    def set_film_classes(self, classes: int):
+        """BRE_OPT_FILM_CLASSES: 1 (one film) or FILM_CLASSES (8 planes per film, see include/bre.h)."""
+        self.set_option(OPT_FILM_CLASSES, int(classes))
+
+    def resolve_classes(self, classes, out):
+        """out (npix, 3) = the sum of the 8 class planes of `classes` ((8 * npix, 3) or (8, npix, 3),
+        torch CUDA float32), added in class order on the context's stream."""
+        npix = out.numel() // 3
+        assert classes.numel() == FILM_CLASSES * 3 * npix
+        self._check(self.lib.bre_resolve_classes(self.h, npix, _ptr(classes), _ptr(out)))
 
     def set_stream(self, stream_handle: int | None):
         self._check(self.lib.bre_set_stream(self.h, stream_handle))

@@ -109,6 +109,8 @@ struct bre_ctx {
     uint64_t sc_hash = 0;  // hash of the uploaded triangles (0: none)
     std::vector<unsigned char> sc_bytes;  // the uploaded triangles' bytes: a hash match is confirmed by memcmp
     DevScene sc_head;      // geometry fields of the uploaded scene
+    DevScene ph_scene_host;                 // the record last copied to ph_scene
+    std::vector<unsigned char> grid_bytes;  // the density grid last copied to grid_dens
     // camera pass
     DevMem cam_dev, cam_perms, cs_o, cs_p, cs_d, cs_t, cs_pix, cs_valid, cam_offs, cam_tmp, cam_flags;
     DevMem seg_o, seg_p, seg_d, seg_t, seg_pix, seg_depth;
@@ -119,6 +121,13 @@ struct bre_ctx {
     bool beams_kept = false;  // in_* hold the current beam set (bre_get_beams)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bre_stats stats;
+    // film classes (BRE_OPT_FILM_CLASSES): 1, or BRE_FILM_CLASSES planes per film; px_cls the class per segment
+    int film_classes = 1;
+    DevMem px_cls;
+    // the passes' own high-priority stream (option 117, PassStream below)
+    int pass_priority = 1;
+    hipStream_t pstream = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
 namespace {
@@ -145,6 +154,44 @@ bre_status set_device(bre_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
     return BRE_OK;
 }
+
+// The photon pass (with its BVH build) and the camera pass run on a stream of the device's highest
+// priority, forked from the caller's stream and joined back to it (option 117, default on): stream
+// order towards the caller is unchanged, but when two contexts pipeline the render (iteration k+1's
+// passes beside iteration k's gather, bench.py --pipeline 1) the dispatcher hands the passes' few
+// workgroups the CUs as the gather's one-wave blocks retire, instead of queueing them behind millions
+// of gather blocks (round 4: k_photons averaged 80 ms in the pipelined trace against 1.4 ms alone).
+struct PassStream {
+    bre_ctx *c;
+    hipStream_t user = nullptr;
+    PassStream(bre_ctx *c_) : c(c_) {
+        if (!c->pass_priority) return;
+        if (!c->pstream) {
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return;
+            if (hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, greatest) != hipSuccess) {
+                c->pstream = nullptr;
+                return;
+            }
+            if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess)
+                return;
+        }
+        if (!c->fork_ev || !c->join_ev) return;
+        if (hipEventRecord(c->fork_ev, c->stream) != hipSuccess ||
+            hipStreamWaitEvent(c->pstream, c->fork_ev, 0) != hipSuccess)
+            return;
+        user = c->stream;
+        c->stream = c->pstream;
+    }
+    ~PassStream() {
+        if (!user) return;
+        // the caller's stream waits for everything the pass queued (also on an early error return)
+        (void)hipEventRecord(c->join_ev, c->pstream);
+        (void)hipStreamWaitEvent(user, c->join_ev, 0);
+        c->stream = user;
+    }
+};
 
 // Build the BVH from device arrays (start/end/radius/power) of n beams.
 bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, const float *radius,
@@ -458,6 +505,10 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         return BRE_OK;
     }
     int kernel = c->kernel;
+    // work-root shards split the tile kernel's work roots: kernels 2 and 5 have none, and would gather
+    // every segment against every beam on every shard (films summing to count x the image)
+    if (c->shard_mode == 2 && c->shard_count > 1 && (kernel == 2 || kernel == 5))
+        return fail(c, BRE_ERR_STATE, "work-root shards (BRE_OPT_SHARD_MODE 2) need the tile kernel (BRE_OPT_KERNEL 0 or 4)");
     if (kernel == 5) {
         if (seg_index) return fail(c, BRE_ERR_STATE, "kernel 5 gathers in the caller's order only");
         return gather_chunk(c, a);
@@ -624,12 +675,18 @@ void bre_destroy(bre_ctx *c) {
                      &c->ss_keys_alt, &c->ss_vals, &c->ss_vals_alt, &c->ss_tmp, &c->ss_o, &c->ss_p, &c->ss_d,
                      &c->ss_t, &c->ss_pix, &c->sp_o, &c->sp_p, &c->sp_d, &c->sp_t, &c->sp_pix, &c->sp_index,
                      &c->gbox, &c->sc_tris, &c->sc_nodes, &c->sc_prims, &c->sc_light_tri, &c->sc_light_func, &c->sc_light_cdf,
-                     &c->px_seg, &c->px_keys, &c->px_keys_alt, &c->px_vals, &c->px_vals_alt, &c->px_tmp,
+                     &c->px_seg, &c->px_keys, &c->px_keys_alt, &c->px_vals, &c->px_vals_alt, &c->px_tmp, &c->px_cls,
                      &c->chk_x, &c->chk_aux, &c->chk_y};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->pstream) {
+        (void)hipStreamSynchronize(c->pstream);
+        (void)hipStreamDestroy(c->pstream);
+    }
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -687,6 +744,11 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_MODE must be 0, 1 or 2");
         c->shard_mode = (int)value;
         return BRE_OK;
+    case BRE_OPT_FILM_CLASSES:
+        if (value != 1 && value != BRE_FILM_CLASSES)
+            return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_FILM_CLASSES must be 1 or %d", BRE_FILM_CLASSES);
+        c->film_classes = (int)value;
+        return BRE_OK;
     case BRE_OPT_SHARD_COUNT:
         if (value < 1 || value > 65536) return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_SHARD_COUNT must be in 1..65536");
         c->shard_count = (int)value;
@@ -738,6 +800,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
                // 2..64 single trace with that many slots per photon (tests: forces the overflow re-trace)
         if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "photon pass mode must be in 0..64");
         c->photon_single = (int)value;
+        return BRE_OK;
+    case 117:  // internal: photon / camera passes on a high-priority stream, 1 (default) / 0 on the caller's (A/B)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "pass priority must be 0 or 1");
+        c->pass_priority = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
@@ -870,9 +936,17 @@ static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
     const float *dd = nullptr;
     if (scene->has_medium == BRE_MEDIUM_GRID) {
         const size_t n = (size_t)scene->grid_n[0] * scene->grid_n[1] * scene->grid_n[2];
-        HIPCHK(c, c->grid_dens.ensure(n * sizeof(float)));
-        HIPCHK(c, hipMemcpyAsync(c->grid_dens.ptr, scene->grid_density, n * sizeof(float), hipMemcpyHostToDevice,
-                                 c->stream));
+        // uploaded only when the density values change (every pass of a render shares one grid)
+        const unsigned char *src = reinterpret_cast<const unsigned char *>(scene->grid_density);
+        const bool same = c->grid_dens.ptr && c->grid_bytes.size() == n * sizeof(float) &&
+                          memcmp(c->grid_bytes.data(), src, n * sizeof(float)) == 0;
+        if (!same) {
+            HIPCHK(c, c->grid_dens.ensure(n * sizeof(float)));
+            HIPCHK(c, hipMemcpyAsync(c->grid_dens.ptr, scene->grid_density, n * sizeof(float), hipMemcpyHostToDevice,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->grid_bytes.assign(src, src + n * sizeof(float));
+        }
         dd = c->grid_dens.as<float>();
     }
     const uint64_t h = hash_triangles(scene);
@@ -910,12 +984,19 @@ static bre_status upload_scene(bre_ctx *c, const bre_scene *scene) {
         const unsigned char *tb = reinterpret_cast<const unsigned char *>(scene_triangles(scene));
         c->sc_bytes.assign(tb, tb + tri_bytes);
     }
-    DevScene ds = c->sc_head;
+    DevScene ds;
+    memcpy(&ds, &c->sc_head, sizeof(DevScene));  // padding bytes included: the record compares bytewise
     prepare_medium(scene, &ds, dd);
-    HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
-    HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &ds, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
-    // the host copies are read by the DMA before the call returns
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the scene record is copied only when it changes: in a render every pass uploads the same record,
+    // and a copy queued behind another context's gather waits for that gather's blocks (round 5 trace:
+    // a 1.6 KB upload took 110 ms in the two-context pipeline)
+    if (!c->ph_scene.ptr || memcmp(&ds, &c->ph_scene_host, sizeof(DevScene)) != 0) {
+        HIPCHK(c, c->ph_scene.ensure(sizeof(DevScene)));
+        HIPCHK(c, hipMemcpyAsync(c->ph_scene.ptr, &ds, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+        // the host copies are read by the DMA before the call returns
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        memcpy(&c->ph_scene_host, &ds, sizeof(DevScene));
+    }
     return BRE_OK;
 }
 
@@ -933,6 +1014,7 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     if (st != BRE_OK) return st;
     st = set_device(c);
     if (st != BRE_OK) return st;
+    PassStream pass(c);
     // an earlier asynchronous gather's device errors are reported before this call changes anything
     st = check_flags(c);
     if (st != BRE_OK) return st;
@@ -1043,6 +1125,7 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     if (st != BRE_OK) return st;
     st = set_device(c);
     if (st != BRE_OK) return st;
+    PassStream pass(c);
     st = check_flags(c);  // an earlier gather's device errors, before this pass changes anything
     if (st != BRE_OK) return st;
     // scene + camera/Halton tables (rebuilt when the scene or film changes)
@@ -1082,7 +1165,7 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
                             c->cam_perms.as<uint16_t>(),
                             width, height, iteration, max_depth, render_surfaces, render_media, cs, d_surface,
                             c->cam_flags.as<unsigned int>(), c->shard_rank, c->shard_count,
-                            c->shard_mode != 0 ? 0 : c->shard_block, c->stream));
+                            c->shard_mode != 0 ? 0 : c->shard_block, c->film_classes, c->stream));
     // total = offs[S-1] + valid[S-1]
     HIPCHK(c, rocprim_free_total_scan(c, cs, nslots, max_depth));
     int64_t last_off = 0;
@@ -1205,6 +1288,10 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
                                   const float *t, const int32_t *pix, float R, int64_t npix, float *d_accum,
                                   float *d_seg_rgb, int32_t *d_seg_counts) {
     const bool sortable = c->kernel == 0 || c->kernel == 4;
+    if (c->film_classes > 1 && d_accum && (!sortable || !c->film_compose))
+        return fail(c, BRE_ERR_STATE, "BRE_OPT_FILM_CLASSES needs the deterministic compose of kernels 0 / 4");
+    if (c->film_classes > 1 && d_accum && (uint64_t)BRE_FILM_CLASSES * (uint64_t)(npix + 1) > 0xffffffffull)
+        return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_FILM_CLASSES: the film is too large for the class keys");
     if (!d_accum || !sortable || n <= 0 || !pix || c->nvalid == 0 || !c->film_compose)
         return gather_segments_core(c, n, o, p, d, t, pix, R, npix, d_accum, d_seg_rgb, d_seg_counts);
     const size_t N = (size_t)n;
@@ -1221,10 +1308,26 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
     HIPCHK(c, c->px_vals_alt.ensure(N * sizeof(int32_t)));
     const size_t tb = pixel_sort_temp_bytes(n);
     HIPCHK(c, c->px_tmp.ensure(tb + 16));
-    DevCounters *ctr = c->counters_buf.as<DevCounters>();  // allocated by the gather above
-    PixelCompose pc{n, pix, segbuf, npix, d_accum, c->px_keys.as<unsigned int>(), c->px_keys_alt.as<unsigned int>(),
-                    c->px_vals.as<int32_t>(), c->px_vals_alt.as<int32_t>(), c->px_tmp.ptr, tb, &ctr->flags,
-                    kFlagPixel};
+    // the flags word of the counter block (a packet shard with no segments never reached the gather's
+    // counters_block, so make sure it exists)
+    if (!c->counters_buf.ptr) {
+        DevCounters *fresh = nullptr;
+        st = counters_block(c, &fresh);
+        if (st != BRE_OK) return st;
+    }
+    DevCounters *ctr = c->counters_buf.as<DevCounters>();
+    const uint8_t *cls = nullptr;
+    if (c->film_classes > 1) {
+        // each segment's class: its packet chunk in the order the gather used (sorted when sorting is on)
+        HIPCHK(c, c->px_cls.ensure(N));
+        const bool sorted = c->sort_segments && n >= 2;
+        HIPCHK(c, launch_seg_classes(n, c->shard_block, c->film_classes, sorted ? c->ss_vals_alt.as<int32_t>() : nullptr,
+                                     c->px_cls.as<uint8_t>(), c->stream));
+        cls = c->px_cls.as<uint8_t>();
+    }
+    PixelCompose pc{n, pix, segbuf, npix, d_accum, cls, c->film_classes, c->px_keys.as<unsigned int>(),
+                    c->px_keys_alt.as<unsigned int>(), c->px_vals.as<int32_t>(), c->px_vals_alt.as<int32_t>(),
+                    c->px_tmp.ptr, tb, &ctr->flags, kFlagPixel};
     HIPCHK(c, launch_pixel_compose(pc, c->stream));
     return BRE_OK;
 }
@@ -1237,6 +1340,15 @@ static bre_status gather_camera(bre_ctx *c, float R, float *d_accum, float *d_se
     return gather_segments(c, c->cam_nseg, c->seg_o.as<float>(), c->seg_p.as<float>(), c->seg_d.as<float>(),
                            c->seg_t.as<float>(), c->seg_pix.as<int32_t>(), R, c->cam_npix, d_accum, d_seg_rgb,
                            d_seg_counts);
+}
+
+bre_status bre_resolve_classes(bre_ctx *c, int64_t npix, const float *d_classes, float *d_out) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (npix < 0 || (npix > 0 && (!d_classes || !d_out))) return fail(c, BRE_ERR_INVALID_ARG, "bre_resolve_classes: bad film");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    HIPCHK(c, launch_resolve_classes(3 * npix, BRE_FILM_CLASSES, d_classes, d_out, c->stream));
+    return BRE_OK;
 }
 
 bre_status bre_gather_camera(bre_ctx *c, float R, float *d_accum) {

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
                                                      float *__restrict__ sd, float *__restrict__ st,
                                                      int32_t *__restrict__ spix, int32_t *__restrict__ valid,
                                                      float *__restrict__ surface, unsigned int *__restrict__ flags,
-                                                     int shard_rank, int shard_count, int shard_block) {
+                                                     int shard_rank, int shard_count, int shard_block, int classes) {
     const DevScene &S = *Sp;
     const DevCamera &C = *Cp;
     const int64_t slot = (int64_t)blockIdx.x * kCamBlock + threadIdx.x;
@@ -498,8 +498,11 @@ __global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict
             for (int c = 0; c < 3; ++c) beta[c] = beta[c] / cp;
         }
     }
-    if (surface && render_surfaces && (!packet_shard || pixel % shard_count == shard_rank))
-        for (int c = 0; c < 3; ++c) surface[3 * pixel + c] += Ld[c];
+    // film classes (BRE_OPT_FILM_CLASSES): pixel p's surface radiance goes to plane p % classes
+    if (surface && render_surfaces && (!packet_shard || pixel % shard_count == shard_rank)) {
+        float *sf = surface + 3 * ((int64_t)(pixel % classes) * C.width * C.height + pixel);
+        for (int c = 0; c < 3; ++c) sf[c] += Ld[c];
+    }
 }
 
 __global__ void k_compact(int64_t nslots_total, const int32_t *__restrict__ valid, const int64_t *__restrict__ offs,
@@ -529,13 +532,13 @@ int64_t camera_slots(int width, int height) {
 hipError_t launch_camera(const DevScene *scene, int stack_depth, const DevCamera *cam, const uint16_t *perms, int width,
                          int height, int iteration, int max_depth, int render_surfaces, int render_media,
                          const CamSlots &s, float *surface, unsigned int *flags, int shard_rank, int shard_count,
-                         int shard_block, hipStream_t stream) {
+                         int shard_block, int classes, hipStream_t stream) {
     const int64_t nslots = camera_slots(width, height);
     if (nslots == 0) return hipSuccess;
     hipLaunchKernelGGL(k_camera, dim3((unsigned)(nslots / kCamBlock)), dim3(kCamBlock),
                        scene_stack_bytes(stack_depth, kCamBlock), stream, scene, cam, perms,
                        iteration, max_depth, render_surfaces, render_media, nslots, s.o, s.p, s.d, s.t, s.pix,
-                       s.valid, surface, flags, shard_rank, shard_count, shard_block);
+                       s.valid, surface, flags, shard_rank, shard_count, shard_block, classes < 1 ? 1 : classes);
     return hipGetLastError();
 }
 

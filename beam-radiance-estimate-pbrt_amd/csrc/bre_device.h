@@ -264,7 +264,9 @@ struct PixelCompose {
     const int32_t *pix;      // [n] pixel of each segment
     const float *seg_rgb;    // [3n] per-segment sums
     int64_t npix;
-    float *accum;            // [3 npix] += per pixel
+    float *accum;            // [3 npix] += per pixel; with classes: [classes][3 npix]
+    const uint8_t *cls;      // [n] film class of each segment (nullptr: one film)
+    int classes;             // 1 or BRE_FILM_CLASSES
     unsigned int *keys, *keys_alt;
     int32_t *vals, *vals_alt;
     void *tmp;
@@ -274,6 +276,11 @@ struct PixelCompose {
 };
 size_t pixel_sort_temp_bytes(int64_t n);
 hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st);
+// film class of each caller-order segment: chunk (sorted position / 64 / block) mod classes; perm[i] =
+// the caller index of sorted segment i (nullptr: unsorted, the caller's order)
+hipError_t launch_seg_classes(int64_t n, int block, int classes, const int32_t *perm, uint8_t *cls, hipStream_t st);
+// out[i] = sum over the classes of in[c][i] in class order, i < m
+hipError_t launch_resolve_classes(int64_t m, int classes, const float *in, float *out, hipStream_t st);
 
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st);
 hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,

@@ -38,25 +38,12 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 // separate libraries): BRE_ABLATE 2 = no exact stage (queue drained unread), 3 = no prefilter scan
 // (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
 // tiles not scanned), 5 = exact stage accumulates in one racy RMW round instead of the ordered rank
-// rounds (wrong sums: the price of the ordering).
-// Exact stage (buffer-load path): 1 = recompute the segment's unit direction instead of loading
-// SegRec plane 2 (default), 0 = load it (A/B)
-#ifndef BRE_AU_RECOMPUTE
-#define BRE_AU_RECOMPUTE 1
-#endif
+// rounds (wrong sums: the price of the ordering).  The variants measured negative in rounds 2-4 (the
+// binary walk, node reload / prefetch, segment values by ds_bpermute, round 3's ranks and LDS float
+// atomics past 8 rounds, the box reject off, pointer loads of SegRec and of the unit direction) were
+// removed in round 5: profiles/r5/negative/ablation_switches.patch restores them.
 #ifndef BRE_ABLATE
 #define BRE_ABLATE 0
-#endif
-// BRE_TREE4 1 (default): the tile kernel walks the 4-wide view of its tree (Node4, k_collapse4);
-// 0: the binary walk, near child first (timing A/B)
-#ifndef BRE_TREE4
-#define BRE_TREE4 1
-#endif
-// BRE_RMW_ROUNDS: exact-stage read-modify-write rounds per batch, 64 (default) = every rank in
-// rounds (queue order, documented operations only); < 64 (timing A/B only) adds the ranks beyond
-// by LDS float atomics, whose same-address order within one instruction is not documented
-#ifndef BRE_RMW_ROUNDS
-#define BRE_RMW_ROUNDS 64
 #endif
 // BRE_NO_QCOUNT / BRE_NO_TAX (timing A/B only): compile out the production queue count / the tile line reject
 #ifndef BRE_NO_QCOUNT
@@ -65,49 +52,30 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_NO_TAX
 #define BRE_NO_TAX 0
 #endif
-// BRE_RANK_MODE (timing A/B only): 0 = verified lane-order ranks (default), 1 = round 3's ds_add_rtn_u32
-// ranks, 2 = the ds_or_rtn_b64 ranks without the order check
-#ifndef BRE_RANK_MODE
-#define BRE_RANK_MODE 0
-#endif
 // BRE_PHASE_TIMING 1 (profiling builds only): the production tile kernel adds, per wave, the
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
 // whole wave into `leaf_visits` (read back with the timing option); the reads serialise a little.
-// BRE_NODE_RELOAD 1: the production instantiation re-reads o, tmax, 1/d from the SegRec at each node
-// visit (register budget, occupancy 7); 0 (default) keeps them in registers at occupancy 6, +1.5% at
-// C2 and C3 once the LPT order made the node loads cheap (explore38)
-#ifndef BRE_NODE_RELOAD
-#define BRE_NODE_RELOAD 0
-#endif
-// BRE_BOX_REJECT 1: the packet-level box reject (bundle_box_miss) joins the line reject at staging
-// BRE_NODE_PREFETCH 1: the traversal requests the next node's record before scanning the pending leaves
-// (measured: no gain, SGPR spills at occupancy 7; profiles/r2/explore/explore22)
-#ifndef BRE_NODE_PREFETCH
-#define BRE_NODE_PREFETCH 0
-#endif
-#ifndef BRE_BOX_REJECT
-#define BRE_BOX_REJECT 1
-#endif
 #ifndef BRE_PHASE_TIMING
 #define BRE_PHASE_TIMING 0
-#endif
-// BRE_EXACT_SHFL 1: the exact stage takes the pair's segment o, tmax, 1/d, au and has_inf from the
-// segment's own lane by ds_bpermute instead of loading three SegRec planes (texture-path relief)
-#ifndef BRE_EXACT_SHFL
-#define BRE_EXACT_SHFL 0
 #endif
 // BRE_SQRT_NOSCALE 1 (default): the exact stage's two square roots without the compiler's small-input
 // scaling (sqrt_cr_noscale, bit-identical results: see tile_exact); 0 = sqrtf
 #ifndef BRE_SQRT_NOSCALE
 #define BRE_SQRT_NOSCALE 1
 #endif
-// BRE_BUF_LOADS 1 (default): the exact stage reads the SegRec planes through a buffer descriptor
-// (SGPR base + 32-bit lane offset: one VALU of address arithmetic instead of 64-bit pointer math;
-// with the power too, C2 +0.8%, C3 +2%, profiles/r3b/run4)
-#ifndef BRE_BUF_LOADS
-#define BRE_BUF_LOADS 1
+// BRE_BUNDLE_LINE 1: the packet bundle line through the centres of the lanes' origin and end-point
+// boxes instead of the mean origin and mean direction (A/B)
+#ifndef BRE_BUNDLE_LINE
+#define BRE_BUNDLE_LINE 0
 #endif
+// BRE_AXIS_BOX 1: the tile axis (k_tile_axis) through the centres of the beams' start and end boxes (A/B)
+#ifndef BRE_AXIS_BOX
+#define BRE_AXIS_BOX 0
+#endif
+// The exact stage reads the SegRec planes through a buffer descriptor (SGPR base + 32-bit lane offset:
+// one VALU of address arithmetic instead of 64-bit pointer math; with the power too, C2 +0.8%, C3 +2%,
+// profiles/r3b/run4).
 // Raw buffer resource over [p, p + 4 GiB): offsets are 32-bit, out-of-range reads return 0.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, -1, 0x00020000);
@@ -251,8 +219,28 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
     const f3 su = mk(wave_sum(valid ? L.au.x : 0.f), wave_sum(valid ? L.au.y : 0.f), wave_sum(valid ? L.au.z : 0.f));
     const float sl = sqrtf(lensq3(su));
     K.omax = wave_max(valid ? L.omax : 0.f);
-    const bool ok = cnt > 0 && sl > 0.f && isfinite(sl);
+    bool ok = cnt > 0 && sl > 0.f && isfinite(sl);
     K.cu = ok ? mk(su.x / sl, su.y / sl, su.z / sl) : mk(0.f, 0.f, 1.f);
+#if BRE_BUNDLE_LINE
+    {
+        // the line through the centres of the origins' and the end points' boxes: closer to the
+        // minimax line than the mean line when the lanes' lengths differ (any line is valid: delta is
+        // measured from it)
+        const auto ctr = [&](float v) {
+            const float hi = wave_max(valid ? v : -FLT_MAX), lo = -wave_max(valid ? -v : -FLT_MAX);
+            return 0.5f * lo + 0.5f * hi;
+        };
+        const f3 a = mk(ctr(L.o.x), ctr(L.o.y), ctr(L.o.z)), b = mk(ctr(L.p.x), ctr(L.p.y), ctr(L.p.z));
+        const f3 ab = sub3(b, a);
+        const float l = sqrtf(lensq3(ab));
+        if (cnt > 0 && l > 1e-6f * (1.f + fabsf(a.x) + fabsf(a.y) + fabsf(a.z)) && isfinite(l) && isfinite(a.x) &&
+            isfinite(a.y) && isfinite(a.z)) {
+            K.co = a;
+            K.cu = mk(ab.x / l, ab.y / l, ab.z / l);
+            ok = true;
+        }
+    }
+#endif
     const auto perp = [&](f3 x) {
         const f3 t = sub3(x, K.co);
         const f3 c = mk(t.y * K.cu.z - t.z * K.cu.y, t.z * K.cu.x - t.x * K.cu.z, t.x * K.cu.y - t.y * K.cu.x);
@@ -482,8 +470,18 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
         return;
     }
     const f3 e = add3(b0, scale3(bu, mb));
+#if BRE_AXIS_BOX
+    // the axis through the centres of the starts' and the ends' boxes (A/B against the means)
+    const auto ctr = [&](float v) {
+        const float hi = wave_max(ok ? v : -FLT_MAX), lo = -wave_max(ok ? -v : -FLT_MAX);
+        return 0.5f * lo + 0.5f * hi;
+    };
+    const f3 ps = mk(ctr(b0.x), ctr(b0.y), ctr(b0.z));
+    const f3 pe = mk(ctr(e.x), ctr(e.y), ctr(e.z));
+#else
     const f3 ps = mk(wave_sum(ok ? b0.x : 0.f) / n, wave_sum(ok ? b0.y : 0.f) / n, wave_sum(ok ? b0.z : 0.f) / n);
     const f3 pe = mk(wave_sum(ok ? e.x : 0.f) / n, wave_sum(ok ? e.y : 0.f) / n, wave_sum(ok ? e.z : 0.f) / n);
+#endif
     f3 d = sub3(pe, ps);
     const float dl = sqrtf(lensq3(d));
     d = (dl > 1e-6f * (1.f + fabsf(ps.x) + fabsf(ps.y) + fabsf(ps.z)) && isfinite(dl)) ? scale3(d, 1.f / dl)
@@ -721,30 +719,6 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     // pass the box test, so the second half is rarely wasted)
     const float4 *sr = seg_plane(srec, seg0 + sl, 0);  // packet-plane layout: plane k at sr[64 k]
     const float4 *rb = reinterpret_cast<const float4 *>(recs + b);
-#if BRE_EXACT_SHFL
-    // the segment's o, tmax, 1/d (sanitised), au and has_inf are resident in lane sl's registers:
-    // fetched by ds_bpermute (LDS crossbar) instead of three of the four SegRec loads (texture path)
-    (void)sd;
-    const int sa = sl << 2;
-    const auto shf = [&](float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(v))); };
-#if BRE_EXACT_SHFL == 3
-    // 3: every segment value by ds_bpermute (no SegRec load at all)
-    (void)sr;
-    const float4 bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
-    const float4 s1 = make_float4(shf(L.p.x), shf(L.p.y), shf(L.p.z), shf(L.mag_a));
-#else
-    const float4 s1 = sr[64], bx = rb[0], by = rb[1], bz = rb[2], bw = rb[3];
-#endif
-    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
-    const float4 s0 = make_float4(shf(L.o.x), shf(L.o.y), shf(L.o.z), shf(L.tmax));
-    const float4 s3 = make_float4(shf(L.invs.x), shf(L.invs.y), shf(L.invs.z), 0.f);
-#if BRE_EXACT_SHFL == 2
-    const float4 s2 = sr[128];  // 2: only the box-test values by ds_bpermute
-#else
-    const float4 s2 = make_float4(shf(L.au.x), shf(L.au.y), shf(L.au.z),
-                                  __int_as_float(__builtin_amdgcn_ds_bpermute(sa, L.has_inf ? 1 : 0)));
-#endif
-#elif BRE_BUF_LOADS
     (void)L;
     (void)sr;
     // SegRec plane k of this packet at byte (seg0 / 64) * 4096 + k * 1024 + sl * 16 (packet-plane layout;
@@ -754,24 +728,14 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec);
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
     const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
-#if BRE_AU_RECOMPUTE
     // au = (p - o) * (1 / |A|) by load_lane's own operations (bit-identical to plane 2, which is not
     // loaded): VALU, which has headroom, for one of the pair's eight vector loads (the texture-data
     // path is the kernel's busiest unit); has_inf from plane 3
     const float4 s1 = buf_f4(srs, vo + 1024u, so_), bz = rb[2], bw = rb[3];
     const f3 au_ = (s1.w != 0.0f) ? div3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s1.w) : mk(0.f, 0.f, 0.f);
     const float4 s2 = make_float4(au_.x, au_.y, au_.z, s3.w);
-#else
-    const float4 s1 = buf_f4(srs, vo + 1024u, so_), s2 = buf_f4(srs, vo + 2048u, so_), bz = rb[2], bw = rb[3];
-#endif
-    // a uniform-radius set's power is in the record's last three words (BeamRec): eight loads per pair
+    // a uniform-radius set's power is in the record's last three words (BeamRec): seven loads per pair
     const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
-#else
-    (void)L;
-    const float4 s0 = sr[0], s3 = sr[192], bx = rb[0], by = rb[1];
-    const float4 s1 = sr[64], s2 = sr[128], bz = rb[2], bw = rb[3];
-    const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
-#endif
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
     const f3 o = mk(s0.x, s0.y, s0.z);
     const float tmax = s0.w;
@@ -856,11 +820,6 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     // That is checked (one ballot); a batch that fails it (never observed) takes its ranks from the
     // final masks instead, after the ORs.  Either way the rank is the lane-order position: the sums
     // are the same bits whatever the hardware's order.
-#if BRE_RANK_MODE == 1  // timing A/B only: round 3's rank (ds_add_rtn_u32: undocumented same-address order)
-    reinterpret_cast<int32_t *>(sh.rkm)[lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    int rank = contrib ? atomicAdd(reinterpret_cast<int32_t *>(sh.rkm) + sl, 1) : 64;
-#else
     sh.rkm[lane] = 0ull;
     __builtin_amdgcn_wave_barrier();
     const unsigned long long lane_bit = 1ull << lane;
@@ -868,11 +827,10 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     if (contrib) before = atomicOr(&sh.rkm[sl], lane_bit);
     int rank = contrib ? __popcll(before) : 64;
     // (a lane's own bit is never in its returned mask: a set bit at or above it means a higher lane went first)
-    if (BRE_RANK_MODE == 0 && __ballot(contrib && (before >> lane) != 0ull) != 0ull) {
+    if (__ballot(contrib && (before >> lane) != 0ull) != 0ull) {
         __builtin_amdgcn_wave_barrier();
         rank = contrib ? lanes_below(sh.rkm[sl]) : 64;
     }
-#endif
     // ranks are dense per segment (0 .. its count - 1): the first rank level no lane holds ends the rounds
     const auto round_k = [&](int k) {
         if (rank == k) {
@@ -890,17 +848,11 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
         round_k(k);
     }
     // a segment repeated more than 8 times in the batch (a transposed tile, few lanes on): the further
-    // rounds, in a loop (BRE_RMW_ROUNDS < 64, timing A/B only: LDS float atomics, undocumented order)
+    // rounds, in a loop
 #pragma nounroll
-    for (int k = 8; k < BRE_RMW_ROUNDS; ++k) {
+    for (int k = 8; k < 64; ++k) {
         if (__ballot(rank == k) == 0ull) return;
         round_k(k);
-    }
-    if (BRE_RMW_ROUNDS < 64 && contrib && rank >= BRE_RMW_ROUNDS) {
-        atomicAdd(&sh.acc[sl].x, v.x);
-        atomicAdd(&sh.acc[sl].y, v.y);
-        atomicAdd(&sh.acc[sl].z, v.z);
-        atomicAdd(&sh.acc[sl].w, v.w);
     }
 }
 
@@ -1056,7 +1008,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             keep = !prefilter ||
                    !((margin ? bundle_far_sep(K, r.b0, T.bu, T.m0, R + r.radius, r.mag_b)
                              : bundle_far(K, r.b0, r.bu, R + r.radius, 0)) ||
-                     (BRE_BOX_REJECT && bundle_box_miss(K, r.box)));
+                     bundle_box_miss(K, r.box));
         }
         const unsigned long long all = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
         const unsigned long long km = __ballot(keep) & all;
@@ -1159,7 +1111,6 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     };
 
     if (__ballot(valid) != 0ull) {
-#if BRE_TREE4
         // Fixed-order walk of the 4-wide view (Node4): a visit tests the four grandchild boxes of a
         // binary node; the leaf tiles it finds are scanned, in slot order, before the walk goes on
         // with the lowest-slot internal child, the others stacked.  (The gather has no early exit, so
@@ -1239,112 +1190,6 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             }
             node = nxt;
         }
-#else
-        const int32_t root = roots[sub];
-        // the production instantiation re-reads the lane's o, tmax and 1/d from its SegRec at each
-        // node visit instead of holding them in VGPRs through the leaf scans (register budget)
-        const int my = (int)(s < nseg ? s : nseg - 1);  // this lane's SegRec (index: one VGPR)
-        // Leaf children found at a node visit are scanned at the top of the next step, c0's before
-        // c1's, so the leaf scan (and the exact stage inside it) is inlined once.
-        int32_t lc0 = 0, lc1 = 0;
-        unsigned long long lm0 = 0ull, lm1 = 0ull;  // lanes on each pending leaf's box (0: none)
-        int node = root;
-        bool have_node = root >= 0;
-        if (!have_node) {
-            lc0 = root;
-            lm0 = __ballot(valid);
-        }
-        int sp = 0;
-        while (true) {
-            // The next node is fixed, and its record requested, BEFORE the pending leaves are scanned
-            // (BRE_NODE_PREFETCH): the record's load latency overlaps the leaf scans.
-            bool more = have_node;
-            if (BRE_NODE_PREFETCH && !have_node && sp > 0) {
-                --sp;
-                node = sh.stk[sp];
-                more = true;
-            }
-            NodeV n{};
-            if (BRE_NODE_PREFETCH && more) {
-                node = __builtin_amdgcn_readfirstlane(node);
-                n = load_node(nodes, node);
-            }
-#pragma nounroll
-            for (int i = 0; i < 2; ++i) {
-                const unsigned long long m = i ? lm1 : lm0;
-                if (m != 0ull) leaf(i ? lc1 : lc0, m);
-            }
-            lm0 = lm1 = 0ull;
-            if (BRE_NODE_PREFETCH) {
-                if (!more) break;
-            } else {
-                if (!have_node) {
-                    if (sp == 0) break;
-                    --sp;
-                    node = sh.stk[sp];
-                }
-                node = __builtin_amdgcn_readfirstlane(node);
-                n = load_node(nodes, node);
-            }
-            if (COUNT) ++visits;
-            const int32_t c0 = n.c0, c1 = n.c1;
-            f3 lo = L.o, li = L.invs;
-            float lt = L.tmax;
-            if (!COUNT && BRE_NODE_RELOAD) {
-                // an opaque copy of the index per visit: keeps the compiler from hoisting the two
-                // loads out of the loop (and the 7 values back into registers)
-                int mi = my;
-                asm volatile("" : "+v"(mi));
-                const float4 *mp = seg_plane(srec, mi, 0);
-                const float4 a0 = mp[0], a3 = mp[192];
-                lo = mk(a0.x, a0.y, a0.z);
-                lt = a0.w;
-                li = mk(a3.x, a3.y, a3.z);
-            }
-            float te0 = 0.f, te1 = 0.f;
-            const bool h0 = valid & (c0 != kEmptyChild) & node_test(n.b0, lo, li, lt, te0);
-            const bool h1 = valid & (c1 != kEmptyChild) & node_test(n.b1, lo, li, lt, te1);
-            const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-            bool go0 = m0 != 0ull, go1 = m1 != 0ull;
-            if (go0 && c0 < 0) {
-                lc0 = c0;
-                lm0 = m0;
-                go0 = false;
-            }
-            if (go1 && c1 < 0) {
-                lc1 = c1;
-                lm1 = m1;
-                go1 = false;
-            }
-            have_node = true;
-            if (go0 && go1) {
-                // near child first, judged by the first lane that enters both
-                const unsigned long long both = m0 & m1;
-                bool first0 = true;
-                if (both != 0ull) {
-                    const int fl = __ffsll((long long)both) - 1;
-                    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te0), fl));
-                    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(te1), fl));
-                    first0 = !(b < a);
-                }
-                const int near = first0 ? c0 : c1, far = first0 ? c1 : c0;
-                if (sp >= stack_cap) {
-                    // never silent: the host turns the flag into BRE_ERR_STATE (bre_api.hip)
-                    if (lane == 0) atomicOr(&ctr->flags, kFlagStack);
-                    break;
-                }
-                sh.stk[sp] = far;
-                ++sp;
-                node = near;
-            } else if (go0) {
-                node = c0;
-            } else if (go1) {
-                node = c1;
-            } else {
-                have_node = false;
-            }
-        }
-#endif
         // drain the prefilter survivors
         __builtin_amdgcn_wave_barrier();
         if (t1 > 0) {
@@ -1730,7 +1575,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     int32_t *pcnt = (counters || a.seg_counts) ? a.pcnt : nullptr;
     if ((counters || a.seg_counts) && !pcnt) return hipErrorInvalidValue;
     if (!a.segrec || a.leaf_size > 64) return hipErrorInvalidValue;
-    if (BRE_TREE4 && !a.nodes4) return hipErrorInvalidValue;  // the 4-wide walk needs the collapsed view
+    if (!a.nodes4) return hipErrorInvalidValue;  // the 4-wide walk needs the collapsed view
     hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
     const TileAxis *tax = nullptr;
@@ -1744,11 +1589,15 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         tax = a.tileax;
     }
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
+    // block map 0 deals S / 8 roots to each XCD: a split that is not a multiple of 8 (work-root shards:
+    // ceil(S / count)) would leave roots unassigned, so such launches take the LPT map
+    GatherArgs am = a;
+    if (am.block_map == 0 && (am.split & 7) != 0) am.block_map = 3;
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nodes4, a.nvalid,        \
                        a.leaf_size,                                                                        \
-                       a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, a.block_map, a.tscan, a.margin, tax)
+                       a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, am.block_map, a.tscan, a.margin, tax)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {

@@ -294,12 +294,16 @@ __global__ __launch_bounds__(kBlock) void k_packet_pick(int64_t n, int64_t m, in
 // let the film differ in the last bits from run to run.  Instead the segments are stably sorted by
 // pixel (so a pixel's segments keep the caller's order: the camera pass's depth order), and one
 // thread per pixel adds its run of segment sums in that order and then adds the run's sum to the film.
+// With film classes (BRE_OPT_FILM_CLASSES) the key is class * (npix + 1) + pixel: a class's pixels in
+// order, each class's slot npix marking an invalid pixel.
 __global__ __launch_bounds__(kBlock) void k_pix_keys(int64_t n, const int32_t *__restrict__ pix, int64_t npix,
+                                                     const uint8_t *__restrict__ cls,
                                                      unsigned int *__restrict__ keys, int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const int32_t p = pix[i];
-    keys[i] = (p < 0 || (int64_t)p >= npix) ? (unsigned int)npix : (unsigned int)p;  // npix: invalid
+    const unsigned int base = cls ? (unsigned int)cls[i] * (unsigned int)(npix + 1) : 0u;
+    keys[i] = base + ((p < 0 || (int64_t)p >= npix) ? (unsigned int)npix : (unsigned int)p);  // npix: invalid
     vals[i] = (int32_t)i;
 }
 
@@ -312,7 +316,8 @@ __global__ __launch_bounds__(kBlock) void k_pix_compose(int64_t n, const unsigne
     if (i >= n) return;
     const unsigned int k = keys[i];
     if (i > 0 && keys[i - 1] == k) return;  // not the first segment of its pixel
-    if ((int64_t)k >= npix) {
+    const int64_t cl = (int64_t)k / (npix + 1), px = (int64_t)k - cl * (npix + 1);
+    if (px >= npix) {
         atomicOr(flags, bad_pixel_flag);  // a seg_pixel outside [0, npix): never silent (check_flags)
         return;
     }
@@ -324,14 +329,48 @@ __global__ __launch_bounds__(kBlock) void k_pix_compose(int64_t n, const unsigne
         b += seg_rgb[3 * s + 2];
     }
     if (r != 0.f || g != 0.f || b != 0.f) {
-        float *a = accum + 3 * (int64_t)k;
+        float *a = accum + 3 * (cl * npix + px);
         a[0] += r;
         a[1] += g;
         a[2] += b;
     }
 }
 
+// The film class of each segment (BRE_OPT_FILM_CLASSES): sorted segment i lies in packet chunk
+// (i / 64) / block -- the unit bre_shard_segments deals to the shards -- and its class is that chunk
+// mod `classes`, written at the segment's caller index.
+__global__ __launch_bounds__(kBlock) void k_seg_classes(int64_t n, int block, int classes,
+                                                        const int32_t *__restrict__ perm, uint8_t *__restrict__ cls) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = perm ? (int64_t)perm[i] : i;
+    cls[s] = (uint8_t)(((i >> 6) / block) % classes);
+}
+
+// The image of the class films, added in class order (bit-identical wherever the planes are).
+__global__ __launch_bounds__(kBlock) void k_resolve_classes(int64_t m, int classes, const float *__restrict__ in,
+                                                            float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    float v = in[i];
+    for (int c = 1; c < classes; ++c) v += in[(int64_t)c * m + i];
+    out[i] = v;
+}
+
 }  // namespace
+
+hipError_t launch_seg_classes(int64_t n, int block, int classes, const int32_t *perm, uint8_t *cls, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_classes, dim3(grid_of(n)), dim3(kBlock), 0, st, n, block < 1 ? 1 : block, classes, perm,
+                       cls);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_classes(int64_t m, int classes, const float *in, float *out, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_resolve_classes, dim3(grid_of(m)), dim3(kBlock), 0, st, m, classes, in, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chunk, const float *o, const float *p,
                               const float *d, const float *t, const int32_t *pix, const int32_t *index, float *o2,
@@ -389,11 +428,13 @@ size_t pixel_sort_temp_bytes(int64_t n) {
 
 hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st) {
     if (c.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pix_keys, dim3(grid_of(c.n)), dim3(kBlock), 0, st, c.n, c.pix, c.npix, c.keys, c.vals);
+    hipLaunchKernelGGL(k_pix_keys, dim3(grid_of(c.n)), dim3(kBlock), 0, st, c.n, c.pix, c.npix, c.cls, c.keys, c.vals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    const uint64_t top = (uint64_t)(c.cls ? c.classes : 1) * (uint64_t)(c.npix + 1);  // keys in [0, top)
+    if (top > 0xffffffffull) return hipErrorInvalidValue;
     int bits = 1;
-    while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)c.npix) ++bits;  // keys in [0, npix]
+    while (bits < 32 && ((uint64_t)1 << bits) < top) ++bits;
     size_t bytes = c.tmp_bytes;
     e = rocprim::radix_sort_pairs(c.tmp, bytes, c.keys, c.keys_alt, c.vals, c.vals_alt, (size_t)c.n, 0, bits, st);
     if (e != hipSuccess) return e;

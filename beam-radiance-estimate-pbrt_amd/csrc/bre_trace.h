@@ -562,7 +562,7 @@ int64_t camera_slots(int width, int height);
 hipError_t launch_camera(const DevScene *scene, int stack_depth, const DevCamera *cam, const uint16_t *perms, int width,
                          int height, int iteration, int max_depth, int render_surfaces, int render_media,
                          const CamSlots &s, float *surface, unsigned int *flags, int shard_rank, int shard_count,
-                         int shard_block, hipStream_t stream);
+                         int shard_block, int classes, hipStream_t stream);
 size_t camera_scan_temp_bytes(int64_t n);
 hipError_t launch_camera_scan(void *tmp, size_t tmp_bytes, const CamSlots &s, int64_t nslots, int max_depth,
                               int64_t *offs, hipStream_t stream);

@@ -21,6 +21,14 @@ segments may then sit on several ranks: the films are partial sums, combined by 
 Work-root shards (bench ``--shard-mode roots``, BRE_OPT_SHARD_MODE 2; the frame is built with
 ``packets=True``): every rank gathers every segment against its share of the BVH work roots, so its
 films are partial sums too and take the same reduce.
+
+Packet-class films (``classes=8``, libbre BRE_OPT_FILM_CLASSES; the bench's default): the film is kept
+as 8 planes -- plane c takes the surface radiance of the pixels p = c (mod 8) and the gather terms of
+the sorted order's packets k = c (mod 8) -- and the image is their sum in class order.  With N ranks
+(N dividing 8) rank r computes exactly the planes c = r (mod N), each bit for bit as one GPU computes
+it (a segment's sum does not depend on which rank gathers its packet), so one GATHER of the ranks'
+planes to the root and the resolve give the one-GPU image bit for bit, where the sum-reduce of partial
+films could not (it adds a pixel's terms in another grouping).
 """
 from __future__ import annotations
 
@@ -49,15 +57,20 @@ class ShardedFrame:
     """Full-resolution RGB accumulation buffer of one rank (only its own tiles are ever written)."""
 
     def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16, block: int = 1,
-                 packets: bool = False):
+                 packets: bool = False, classes: int = 1):
         import torch
 
         self.w, self.h, self.rank, self.world, self.tile, self.block = w, h, rank, world, tile, block
         # packets=True: PACKET shards (BRE_OPT_SHARD_MODE 1) -- every rank may write every pixel (its
-        # range of the sorted segment packets), and the films are SUMMED by one reduce
+        # range of the sorted segment packets), and the films are SUMMED by one reduce, or, with
+        # classes=8 (packet-class films), gathered plane by plane
         self.packets = packets
+        if classes != 1 and not packets:
+            raise ValueError("packet-class films need packet shards")
+        self.classes = classes
         self.pixels = np.arange(w * h, dtype=np.int64) if packets else tile_pixels(w, h, rank, world, tile, block)
-        self.accum = torch.zeros((w * h, 3), dtype=torch.float32, device=device)
+        # with classes: (classes * w * h, 3), plane c = rows [c * w * h, (c + 1) * w * h)
+        self.accum = torch.zeros((classes * w * h, 3), dtype=torch.float32, device=device)
         self.device = device
         self._band = None
         if not packets:  # the band machinery (also at world 1: a live 1-rank group still runs the gather)
@@ -108,6 +121,8 @@ class ShardedFrame:
         live = dist.is_available() and dist.is_initialized()
         if self.world == 1 and not live:
             return self.accum
+        if self.packets and self.classes > 1 and self.classes % self.world == 0:
+            return self._gather_planes(root)
         if self.packets:  # partial films of one image: one sum-reduce to the root
             if dist.get_backend() == "gloo" and self.accum.is_cuda:  # gloo reduces host tensors
                 host = self.accum.cpu()
@@ -122,9 +137,49 @@ class ShardedFrame:
             self.scatter_bands(parts, skip=root)
         return self.accum
 
+    def owned_planes(self, rank: int | None = None):
+        """The class planes rank `rank` (default: this rank) computes: c = rank (mod world)."""
+        r = self.rank if rank is None else rank
+        return [c for c in range(self.classes) if c % self.world == r]
+
+    def plane(self, c: int):
+        n = self.w * self.h
+        return self.accum[c * n:(c + 1) * n]
+
+    def _gather_planes(self, root: int):
+        """Packet-class films: each rank's own planes (classes / world of them, contiguous) gathered to
+        the root, which writes them into its planes -- every plane as the rank that owns it computed it."""
+        import torch
+        import torch.distributed as dist
+
+        mine = torch.cat([self.plane(c) for c in self.owned_planes()])
+        host = dist.get_backend() == "gloo" and mine.is_cuda  # gloo gathers host tensors
+        send = mine.cpu() if host else mine
+        parts = [torch.empty_like(send) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(send, gather_list=parts, dst=root)
+        if self.rank == root:
+            n = self.w * self.h
+            for r, part in enumerate(parts):
+                if r == root:
+                    continue
+                for k, c in enumerate(self.owned_planes(r)):
+                    self.plane(c).copy_(part[k * n:(k + 1) * n].to(self.accum.device))
+        return self.accum
+
+    def resolve(self):
+        """The image of a packet-class film: the planes added in class order (plane 0 + plane 1 + ...,
+        the order bre_resolve_classes uses), on the root after gather_to_root(); the film itself without
+        classes."""
+        if self.classes == 1:
+            return self.accum
+        out = self.plane(0).clone()
+        for c in range(1, self.classes):
+            out += self.plane(c)
+        return out
+
     # the round-1 name (a reduce of full frames); kept as an alias of the gather
     reduce_to_root = gather_to_root
 
     def image(self, iteration: int):
         """L = Ld / (iter + 1)  (photonbeam.cpp:578), on the root after gather_to_root()."""
-        return self.accum / float(iteration + 1)
+        return self.resolve() / float(iteration + 1)

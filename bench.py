@@ -57,6 +57,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NODE4_BYTES = 128.0     # one visit of the tile kernel's 4-wide walk reads one Node4 record (bre_device.h)
 CUS, SIMDS = 256, 4     # VALU issue peak: one wave64 instruction per 2 clocks per SIMD-32
 
 
@@ -97,6 +98,11 @@ def parse(argv=None):
     ap.add_argument("--split-records", type=int, default=-1, help=argparse.SUPPRESS)  # BeamRec layout A/B (option 113)
     ap.add_argument("--film-compose", type=int, default=-1, help=argparse.SUPPRESS)  # film accumulation A/B (option 114)
     ap.add_argument("--photon-single", type=int, default=-1, help=argparse.SUPPRESS)  # photon pass form A/B (option 116)
+    ap.add_argument("--pass-priority", type=int, default=-1, help=argparse.SUPPRESS)  # option 117 A/B
+    ap.add_argument("--film-classes", type=int, default=1,
+                    help="packet shards: keep the film as 8 packet-class planes, gathered and resolved in class "
+                         "order, so every N dividing 8 renders the one-GPU film bit for bit (0: one film, "
+                         "sum-reduced)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
@@ -121,6 +127,10 @@ def parse(argv=None):
                          "boundary: the same segments in the reference's recorder order (16x16 tiles dealt to 16 "
                          "threads, each pixel's depths in order) through bre_gather_device, the C-ABI entry the "
                          "pbrt adapter uses")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="c2: skip the untimed-by-headline C3 (N=1) and C4 (every N) iteration-0 legs")
+    ap.add_argument("--c4-leg", choices=["auto", "on", "off"], default="auto",
+                    help="c2: the C4 iteration-0 gather leg (auto: with strong scaling, at every N)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--progress", action="store_true",
                     help="print a line per timed step to stderr (synchronises each step; long C4/C5 runs)")
@@ -201,8 +211,9 @@ def main():
     srank, scount = (rank, world) if strong else (0, 1)
     if args.emulate_shard and world == 1:  # one rank's share of an N-GPU strong-scaling run, on this GPU
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
+    classes = film_classes(args)
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
-                              packets=args.shard_mode in ("packets", "roots"))
+                              packets=args.shard_mode in ("packets", "roots"), classes=classes)
     def make_ctx():
         return make_context(bre, args, dev)
 
@@ -248,6 +259,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # the rendered film's bits (root): with packet-class films the same for every N dividing 8
+    digest = film_digest(frame) if (rank == 0 and args.workload != "synthetic" and not args.emulate_shard) else None
     gather_per_step = [a.elapsed_time(b) for a, b in events]
     gather_ms = float(np.mean(gather_per_step))
     if world > 1:
@@ -263,15 +276,15 @@ def main():
     value = total_seg / elapsed
 
     # untimed: one more step with counters and per-phase HIP-event timing inside libbre, at iteration 0
-    # (the largest radius: the roofline's launch) and at the last timed step's iteration (the smallest
-    # radius the line times: the scan-bound end of the render)
+    # (the largest radius: the roofline's launch) and at the smallest-radius iteration the line times
+    # (the scan-bound end of the render: C2 iteration 15 whenever --steps >= 16)
     diag, st, st_last = {}, None, None
     if not args.no_diag:
         g.set_option(bre.OPT_COUNTERS, 1)
         g.set_option(bre.OPT_TIMING, 1)
         diag = wl.diagnostics(0)
         st = g.stats()
-        k_last = args.steps - 1
+        k_last = late_step(wl, args.steps)
         if getattr(wl, "iteration", None) and wl.iteration(k_last) != wl.iteration(0):
             d_last = wl.diagnostics(k_last)
             st_last = g.stats()
@@ -295,6 +308,7 @@ def main():
         "dtype": "fp32",
         "data": wl.data,
         "config": wl.config(world),
+        "film_digest": digest,
         "estimates_per_step_per_gpu": nseg_local / args.steps,
         "gather_kernel_ms": gather_ms,
         "gather_ms_per_step": gather_per_step if rank == 0 else None,
@@ -303,7 +317,7 @@ def main():
         result.update(counter_block(st, args))
         result["candidate_pair_tests_per_s"] = result["candidates_per_estimate"] * value
     if st_last is not None:
-        # the same counter block at the last timed iteration (the late, small-radius
+        # the same counter block at the smallest-radius timed iteration (the late
         # iterations are scan-bound and their funnel belongs in the line)
         last = counter_block(st_last, args)
         last.update({"iteration": st_last["_iteration"], "gather_ms": st_last["_gather_ms"]})
@@ -323,6 +337,17 @@ def main():
         result["roofline"] = roofline(st, args, wl, gather_per_step[0], pmc, cpu)
     wl.close()
     g.close()
+    # the other BASELINE configurations, outside the headline's timed region: C3's
+    # iteration 0 on rank 0 at N = 1, and C4's iteration-0 gather on every rank (max over ranks), so an
+    # N-GPU run also measures the north star's scaling configuration
+    if args.workload == "c2" and not args.no_legs and not args.emulate_shard:
+        legs = {}
+        if world == 1 and rank == 0:
+            legs["c3"] = config_leg(args, bre, dmod, dev, "c3", 1, 0)
+        if args.c4_leg == "on" or (args.c4_leg == "auto" and args.scaling == "strong"):
+            legs["c4"] = config_leg(args, bre, dmod, dev, "c4", world, rank)
+        if rank == 0:
+            result["config_legs"] = legs
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
@@ -331,6 +356,84 @@ def main():
                 f.write(line + "\n")
     if world > 1:
         dist.destroy_process_group()
+
+
+def film_classes(args):
+    """Packet-class films (libbre BRE_OPT_FILM_CLASSES, dist.ShardedFrame classes): on with packet
+    shards (the default), so the N-GPU film is the one-GPU film bit for bit for every N dividing 8."""
+    return 8 if (args.shard_mode == "packets" and args.film_classes and args.workload != "synthetic") else 1
+
+
+def film_digest(frame):
+    """sha256 of the resolved film's float32 bits and the film's sum (what the root holds after the
+    timed steps): equal digests across N = 1, 2, 4, 8 show the split changes no bit."""
+    import hashlib
+
+    img = frame.resolve().detach().to("cpu").contiguous().numpy()
+    return {"sha256": hashlib.sha256(img.tobytes()).hexdigest()[:32], "sum": float(img.astype(np.float64).sum()),
+            "classes": frame.classes, "pixels": int(img.shape[0])}
+
+
+def late_step(wl, steps):
+    """The timed step of the smallest radius: the largest iteration the line times (C2 iteration 15
+    whenever --steps >= 16; the last step when the workload has no iteration schedule)."""
+    if not getattr(wl, "iteration", None):
+        return steps - 1
+    return max(range(steps), key=lambda k: (wl.iteration(k), -k))
+
+
+def config_leg(args, bre, dmod, dev, name, world, rank):
+    """One iteration (iteration 0, the largest radius) of BASELINE configuration `name` on a fresh
+    context: photon pass + build, camera pass, and the gather of this rank's share of the sorted segment
+    packets, the gather timed by HIP events on its stream.  With N ranks: the gather time is the max over
+    ranks, the estimates their sum, and the partial films are reduced to rank 0 (one RCCL reduce).
+    Errors are reported in the leg, never raised (the headline line stands on its own)."""
+    import argparse as ap_
+    import torch
+    import torch.distributed as dist
+
+    try:
+        a = ap_.Namespace(**vars(args))
+        preset = WORKLOADS[name]
+        a.workload, a.photons, a.width, a.height, a.steps = name, preset["photons"], preset["width"], preset["height"], 1
+        a.entry, a.shard_mode = "camera", "packets"
+        frame = dmod.ShardedFrame(a.width, a.height, rank, world, device=dev, block=1, packets=True,
+                                  classes=film_classes(a))
+        c, st = make_context(bre, a, dev)
+        wl = SceneWorkload(a, bre, [(c, st)], frame, rank, world)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        n = wl.step(0, ev, scratch=False)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        gms = ev[0].elapsed_time(ev[1])
+        nb = int(wl.nbeams)
+        if world > 1:
+            cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+            tt = torch.tensor([gms, wall], dtype=torch.float64, device=cdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            gms, wall = float(tt[0]), float(tt[1])
+            tot = torch.tensor([n], dtype=torch.int64, device=cdev)
+            dist.all_reduce(tot)
+            n_all = int(tot.item())
+            frame.gather_to_root(0)
+            torch.cuda.synchronize(dev)
+        else:
+            n_all = n
+        wl.close()
+        c.close()
+        return {"workload": f"{name.upper()} iteration 0 ({preset['photons'] / 1e6:g}M photons, {a.width}x{a.height}, "
+                            f"{'grid-density smoke, g 0.7' if preset['medium'] == 'smoke' else 'homogeneous fog'})",
+                "n_gpus": world, "estimates": n_all, "beams": nb,
+                "gather_ms": gms, "gather_estimates_per_s": n_all / (gms * 1e-3),
+                "iteration_ms": wall * 1e3, "iteration_estimates_per_s": n_all / wall,
+                "timing": "gather: HIP events around the tile kernel launch on its stream, max over ranks; "
+                          "iteration: wall time of photon pass + build + camera pass + gather, max over ranks"}
+    except Exception as e:  # reported, never fatal to the headline line
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def make_context(bre, args, dev):
@@ -347,9 +450,11 @@ def make_context(bre, args, dev):
     for opt, val in ((102, args.occupancy if args.occupancy else -1), (bre.OPT_TILE_LEAF, args.tile_leaf or -1),
                      (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
                      (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose),
-                     (116, args.photon_single)):
+                     (116, args.photon_single), (117, args.pass_priority)):
         if val >= 0:
             c.set_option(opt, val)
+    if film_classes(args) > 1:
+        c.set_film_classes(bre.FILM_CLASSES)
     st = torch.cuda.Stream(dev)
     c.set_stream(st.cuda_stream)
     return c, st
@@ -388,7 +493,8 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     nseg = max(st["n_segments"], 1)
     items = (nseg + 63) // 64 * args.split
     # what the packet algorithm requests from the memory hierarchy per launch (L1 / TA level): every
-    # visited node line and staged beam line (64 B each) of every (packet, subtree) item; per item the
+    # visited node record (the 4-wide walk's 128-B Node4; node_visits counts its visits) and staged beam
+    # line (64 B) of every (packet, subtree) item; per item the
     # segments (40 B in) and the per-subtree partial sums (12 B out) of its 64 lanes; per queued
     # (lane, beam) pair the exact stage's loads (three of the segment's 16-B SegRec planes -- the unit
     # direction is recomputed -- and the 64-B BeamRec, which carries the power of the photon pass's
@@ -396,13 +502,14 @@ def roofline(st, args, wl, gather_ms, pmc, cpu):
     # split in, 12 B out per segment)
     queued = st.get("queued_pairs", 0)
     pair_b = 128.0 if args.split_records == 1 else 112.0
-    req = (64.0 * (st["node_visits"] + st["beam_evals"]) + items * 64 * (40 + 12) + pair_b * queued
+    req = (NODE4_BYTES * st["node_visits"] + 64.0 * st["beam_evals"] + items * 64 * (40 + 12) + pair_b * queued
            + nseg * 12 * (args.split + 1))
     requested = req / (gather_ms * 1e-3) / 1e9
     hbm = {"requested_GBps": requested, "peak": HBM_PEAK_GBPS, "requested_over_peak": requested / HBM_PEAK_GBPS,
            "requested_bytes_per_launch": req, "queued_pairs_per_launch": queued,
-           "requested_model": "bytes the packets request at the L1 / texture-address level: 64 B x (node "
-                              "visits + beam lines staged) + 52 B x 64 per (packet, subtree) item + "
+           "requested_model": "bytes the packets request at the L1 / texture-address level: 128 B x node "
+                              "visits (4-wide Node4 records) + 64 B x beam lines staged + 52 B x 64 per (packet, "
+                              "subtree) item + "
                               f"{pair_b:.0f} B per queued exact-stage pair + 12 B x (split + 1) per segment; counts "
                               "from this run's counter pass.  Served mostly by L1 / L2 / Infinity Cache: compare "
                               "traffic_bytes_per_launch (HBM) and the l2 block"}
@@ -807,7 +914,7 @@ def host_threads():
 
 def cpu_baseline(wl, args, gather_per_step):
     """Oracle = CPU restatement of the reference algorithm (not pbrt itself: the reference build was
-    denied).  For the first and the last timed iteration: the SAH build single-threaded
+    denied).  For iteration 0 and the smallest-radius timed iteration: the SAH build single-threaded
     (as photonbeambvh.cpp:232), then the gather of a random sample of that iteration's segments on
     every host thread this process may use (256-segment chunks pulled dynamically, like
     ParallelFor2D, parallel.cpp:247-299) and on 1 thread.  value = 1 / the mean over the sampled
@@ -817,7 +924,7 @@ def cpu_baseline(wl, args, gather_per_step):
 
     ora = load_oracle()
     threads, cpu_note = host_threads()
-    iters = sorted({0, wl.iteration(args.steps - 1)}) if wl.name != "synthetic" else [0]
+    iters = sorted({0, wl.iteration(late_step(wl, args.steps))}) if wl.name != "synthetic" else [0]
     per_it, visit, cand = [], [], []
     for it in iters:
         beams, segs, R = wl.cpu_inputs(it)
@@ -866,8 +973,8 @@ def cpu_baseline(wl, args, gather_per_step):
             "kind": "port",
             "value_1_thread": value1,
             "threads_note": cpu_note,
-            "sample": (f"random camera segments of the {wl.name} workload at iterations {iters} (the first and last "
-                       f"timed iterations), gathered against all of that iteration's beams through the oracle's SAH "
+            "sample": (f"random camera segments of the {wl.name} workload at iterations {iters} (the largest and "
+                       f"smallest radius the line times), gathered against all of that iteration's beams through the oracle's SAH "
                        f"tree: {threads} threads (every CPU this process may use: {cpu_note}; nproc {os.cpu_count()}) "
                        f"and 1 thread; value = 1 / mean seconds per estimate over those iterations"),
             "per_iteration": per_it,

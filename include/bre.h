@@ -93,7 +93,7 @@ typedef enum bre_option {
     BRE_OPT_SHARD_BLOCK = 14, /* tile shards: tiles per side of the blocks dealt to the shards; packet
                                 shards: consecutive packets per chunk dealt to the shards (1..4096,
                                 default 1) */
-    BRE_OPT_SHARD_MODE = 15  /* 0 (default): shards own image tiles (SHARD_BLOCK), each pixel is written
+    BRE_OPT_SHARD_MODE = 15, /* 0 (default): shards own image tiles (SHARD_BLOCK), each pixel is written
                                 by one shard.  1: PACKET shards -- every shard runs the whole camera
                                 pass and gathers its round-robin share of the sorted 64-segment packets
                                 (bre_shard_segments); the surface radiance of pixel p is added by shard
@@ -102,7 +102,19 @@ typedef enum bre_option {
                                 gathers every segment against the BVH work roots rank, rank + count, ...
                                 of the size-ordered list (kernels 0/4); surface radiance and films as
                                 in 1, per-segment outputs are the shard's subtrees' partial sums */
+    BRE_OPT_FILM_CLASSES = 16 /* 1 (default) or BRE_FILM_CLASSES (8): the films the camera pass and the
+                                kernel 0 / 4 gathers add to are 8 planes of float[3*npix] -- class c
+                                holds the surface radiance of the pixels p with p % 8 == c and the
+                                gather terms of the segments in the sorted order's packet chunks k
+                                (BRE_OPT_SHARD_BLOCK packets each) with k % 8 == c, each pixel's
+                                segments of a class added in the caller's order.  The image is the sum
+                                of the planes in class order (bre_resolve_classes).  Packet shard r of
+                                count (count dividing 8) computes exactly classes c % count == r, so
+                                gathering the shards' planes and resolving gives the 1-shard image
+                                bit for bit (dist.py ShardedFrame, bench.py --gpus N). */
 } bre_option;
+
+#define BRE_FILM_CLASSES 8
 
 typedef struct bre_stats {
     int64_t n_beams;         /* beams in the current set (after set_beams) */
@@ -161,7 +173,12 @@ bre_status bre_set_beams_device(bre_ctx *ctx, int64_t n, const float *d_start_xy
 /* ---- gather (replaces photonbeam.cpp:494-508 for every segment of an iteration) ----
    seg_o_xyz, seg_p_xyz, seg_d_xyz: float[3*nseg] (ray.o, isect.p, ray.d); seg_tmax: float[nseg]
    (ray.tMax); seg_pixel: int32[nseg], pixel index in [0, npix).
-   accum_rgb: float[3*npix], accumulated (+=) like PhotonBeamPixel::Ld (may be NULL).
+   accum_rgb: float[3*npix], accumulated (+=) like PhotonBeamPixel::Ld (may be NULL).  Kernels 0 / 4
+   add deterministically: the per-segment sums are sorted by pixel (stable, so a pixel's segments
+   keep the caller's order) and one thread per pixel adds its segments in that order, then adds the
+   total to the pixel once.  That pass is O(segments) in all, but a pixel's run is serial: callers
+   whose segments pile onto a few pixels (thousands per pixel) pay that run's length in one thread;
+   camera-pass segments have at most maxdepth (+ null crossings) per pixel.
    seg_rgb: float[3*nseg] per-segment sums, overwritten (may be NULL).
    seg_counts: int32[2*nseg] per-segment {C candidates, contributions} (may be NULL).  With
    BRE_OPT_COUNTERS=1 both are counted (C by an extra box test of every visited beam); without it
@@ -186,6 +203,11 @@ bre_status bre_gather_device(bre_ctx *ctx, int64_t nseg, const float *d_seg_o_xy
                              const float *d_seg_tmax, const int32_t *d_seg_pixel,
                              float beam_radius_cur, int64_t npix, float *d_accum_rgb,
                              float *d_seg_rgb, int32_t *d_seg_counts);
+
+/* The image of BRE_OPT_FILM_CLASSES films: out[i] = classes[0][i] + ... + classes[7][i] for the
+   3*npix floats i, added in class order (device pointers; asynchronous on the context's stream).
+   out may alias classes[0]. */
+bre_status bre_resolve_classes(bre_ctx *ctx, int64_t npix, const float *d_classes, float *d_out);
 
 /* ---- multi-GPU gather (SURVEY.md §8(b) `bre_gather_sharded`, §8(e)) ----
    ctxs[0 .. n_ctx): one context per GPU (several contexts on one device are allowed: tests), each

@@ -356,6 +356,40 @@ class BeamBVH {
         if (visited) *visited = v;
         return beams;
     }
+    // The same depth-first walk as intersect(), handing each leaf beam to f in the order intersect()
+    // would return it, without building the per-query vector<shared_ptr> (image-parity mode, below).
+    template <class F>
+    void forEachCandidate(const Ray &ray, F &&f, int64_t *visited) const {
+        if (nodes.empty()) return;
+        V3 invDir(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+        int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+        int toVisitOffset = 0, currentNodeIndex = 0;
+        int nodesToVisit[64];
+        int64_t v = 0;
+        while (true) {
+            const LinearNode *node = &nodes[currentNodeIndex];
+            ++v;
+            if (intersectP(node->bounds, ray, invDir, dirIsNeg)) {
+                if (node->nPhotonBeams > 0) {
+                    for (int i = 0; i < node->nPhotonBeams; ++i) f(*photonBeams[node->photonBeamsOffset + i]);
+                    if (toVisitOffset == 0) break;
+                    currentNodeIndex = nodesToVisit[--toVisitOffset];
+                } else {
+                    if (dirIsNeg[node->axis]) {
+                        nodesToVisit[toVisitOffset++] = currentNodeIndex + 1;
+                        currentNodeIndex = node->secondChildOffset;
+                    } else {
+                        nodesToVisit[toVisitOffset++] = node->secondChildOffset;
+                        currentNodeIndex = currentNodeIndex + 1;
+                    }
+                }
+            } else {
+                if (toVisitOffset == 0) break;
+                currentNodeIndex = nodesToVisit[--toVisitOffset];
+            }
+        }
+        if (visited) *visited = v;
+    }
     size_t nodeCount() const { return nodes.size(); }
     size_t beamCount() const { return photonBeams.size(); }
     int maxLeafSize() const {
@@ -512,6 +546,57 @@ static void gatherSegment(const BeamBVH &bvh, V3 o, V3 p, V3 d, Float tMax, Floa
     if (contrib) *contrib = nc;
 }
 
+// Image-parity mode (tests only: whole films at BASELINE sizes, where the reference form takes tens
+// of minutes).  The candidates come in the reference's DFS order and every candidate that can
+// contribute goes through beamContribution exactly as above, so the sums and counts are ora_gather's
+// bit for bit.  A candidate is skipped without ComputeClosestPoints only when the double-precision
+// distance D between the segment's LINE and the beam's LINE exceeds MaxDistance by 1e-4 (1 + the
+// coordinate scale): the reference's aClosest lies on segment A and its bClosest on beam B's line
+// (also in the t1 quirk of photonbeam.cpp:178-181), each to within a few float ulps of the
+// coordinates and of |t1| <= |t| / |n| (<= 100 x the scale for |n| >= 0.01, the only pairs skipped),
+// so its float distance is >= D - 1e-5 (1 + scale) > MaxDistance: such a pair never contributes.
+static void gatherSegmentSkip(const BeamBVH &bvh, V3 o, V3 p, V3 d, Float tMax, Float R, Float *acc,
+                              int64_t *cand, int64_t *vis, int64_t *contrib, int64_t *skipped) {
+    Ray ray{o, d, tMax};
+    int64_t v = 0, nc = 0, nk = 0, ns = 0;
+    const double ax = (double)p.x - o.x, ay = (double)p.y - o.y, az = (double)p.z - o.z;
+    const double al = std::sqrt(ax * ax + ay * ay + az * az);
+    const double osc = std::max(std::max(std::fabs((double)o.x), std::fabs((double)o.y)), std::fabs((double)o.z)) + al;
+    bvh.forEachCandidate(ray, [&](const PhotonBeam &beam) {
+        ++nc;
+        const double bx = (double)beam.end.x - beam.start.x, by = (double)beam.end.y - beam.start.y,
+                     bz = (double)beam.end.z - beam.start.z;
+        const double bl = std::sqrt(bx * bx + by * by + bz * bz);
+        if (al > 0 && bl > 0) {
+            const double ux = ax / al, uy = ay / al, uz = az / al, vx = bx / bl, vy = by / bl, vz = bz / bl;
+            const double nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+            const double nl = std::sqrt(nx * nx + ny * ny + nz * nz);
+            if (nl >= 0.01) {
+                const double tx = (double)beam.start.x - o.x, ty = (double)beam.start.y - o.y,
+                             tz = (double)beam.start.z - o.z;
+                const double D = std::fabs(tx * nx + ty * ny + tz * nz) / nl;
+                const double bsc = std::max(std::max(std::fabs((double)beam.start.x), std::fabs((double)beam.start.y)),
+                                            std::fabs((double)beam.start.z)) + bl;
+                if (D > (double)(R + beam.radius) + 1e-4 * (1.0 + osc + bsc)) {
+                    ++ns;
+                    return;
+                }
+            }
+        }
+        Float rgb[3];
+        if (beamContribution(beam, o, p, R, rgb)) {
+            acc[0] += rgb[0];
+            acc[1] += rgb[1];
+            acc[2] += rgb[2];
+            ++nk;
+        }
+    }, &v);
+    if (cand) *cand = nc;
+    if (vis) *vis = v;
+    if (contrib) *contrib = nk;
+    if (skipped) *skipped = ns;
+}
+
 }  // namespace ora
 
 using namespace ora;
@@ -651,6 +736,39 @@ void ora_gather(void *hp, int64_t nseg, const float *o, const float *p, const fl
     };
     std::vector<std::thread> pool;
     for (int t = 0; t < nthreads; ++t) pool.emplace_back(worker);
+    for (auto &t : pool) t.join();
+}
+
+// The image-parity gather (gatherSegmentSkip): ora_gather's per-segment sums, candidate and
+// contribution counts bit for bit, on nthreads threads; seg_skip (optional) counts the candidates
+// skipped by the line-distance proof.  Films are composed by the caller in segment order.
+void ora_gather_skip(void *hp, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
+                     float R, float *seg_rgb, int64_t *seg_cand, int64_t *seg_contrib, int64_t *seg_skip,
+                     int nthreads) {
+    Handle *h = (Handle *)hp;
+    const BeamBVH &bvh = *h->bvh;
+    std::atomic<int64_t> next(0);
+    const int64_t chunk = 64;
+    auto worker = [&]() {
+        while (true) {
+            const int64_t s0 = next.fetch_add(chunk);
+            if (s0 >= nseg) break;
+            const int64_t s1 = std::min(nseg, s0 + chunk);
+            for (int64_t s = s0; s < s1; ++s) {
+                Float acc[3] = {0, 0, 0};
+                int64_t c, v, k, sk;
+                gatherSegmentSkip(bvh, ld3(o, s), ld3(p, s), ld3(d, s), tmax[s], R, acc, &c, &v, &k, &sk);
+                if (seg_rgb) {
+                    seg_rgb[3 * s] = acc[0]; seg_rgb[3 * s + 1] = acc[1]; seg_rgb[3 * s + 2] = acc[2];
+                }
+                if (seg_cand) seg_cand[s] = c;
+                if (seg_contrib) seg_contrib[s] = k;
+                if (seg_skip) seg_skip[s] = sk;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, nthreads); ++t) pool.emplace_back(worker);
     for (auto &t : pool) t.join();
 }
 

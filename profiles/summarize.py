@@ -29,9 +29,13 @@ def main(d, out):
     if os.path.exists(trace):
         for r in csv.DictReader(open(trace)):
             k = short(r["Kernel_Name"])
-            if "gather" in k and k in res:
+            if ("gather" in k or "k_photons" in k or "k_camera" in k) and k in res:
                 ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
                 res[k].setdefault("dispatch_ms", []).append(round(ms, 3))
+    for v in res.values():  # the passes' medians (round 5: pipelined passes beside the gather)
+        if v.get("dispatch_ms"):
+            srt = sorted(v["dispatch_ms"])
+            v["median_dispatch_ms"] = srt[len(srt) // 2]
     for cname, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):

@@ -39,6 +39,7 @@ class Oracle:
         lib.ora_bvh_max_leaf.restype = I32
         lib.ora_bvh_free.argtypes = [P]
         lib.ora_gather.argtypes = [P, I64, P, P, P, P, P, F, P, P, P, P, P, I32, I64]
+        lib.ora_gather_skip.argtypes = [P, I64, P, P, P, P, F, P, P, P, P, I32]
         lib.ora_gather_bruteforce.argtypes = [I64, P, P, P, P, I32, I64, P, P, P, P, F, P, P, P, I32, P]
         U64 = ctypes.c_uint64
         lib.ora_trace_photons.argtypes = [P, I64, I32, I32, F, I64, P, P, P, P, P]
@@ -333,6 +334,25 @@ class OracleBVH:
                                 _p(rgb), _p(accum), _p(cand), _p(vis), _p(contrib), int(nthreads), int(chunk))
         out = {"seg_rgb": rgb, "cand": cand, "visit": vis, "contrib": contrib}
         if accum is not None:
+            out["accum"] = accum
+        return out
+
+    def gather_skip(self, segs, R, npix=None, nthreads=1):
+        """Image-parity gather (ora_gather_skip): gather()'s per-segment sums and counts bit for bit,
+        with candidates that provably cannot contribute skipped before ComputeClosestPoints; the film
+        (npix) is composed here from the per-segment sums, in segment order."""
+        s = {k: np.ascontiguousarray(segs[k], np.float32) for k in ("o", "p", "d", "tmax")}
+        ns = s["tmax"].shape[0]
+        rgb = np.zeros((ns, 3), np.float32)
+        cand = np.zeros(ns, np.int64)
+        contrib = np.zeros(ns, np.int64)
+        skip = np.zeros(ns, np.int64)
+        self.ora.lib.ora_gather_skip(self.h, ns, _p(s["o"]), _p(s["p"]), _p(s["d"]), _p(s["tmax"]), float(R),
+                                     _p(rgb), _p(cand), _p(contrib), _p(skip), int(nthreads))
+        out = {"seg_rgb": rgb, "cand": cand, "contrib": contrib, "skipped": skip}
+        if npix is not None:
+            accum = np.zeros((npix, 3), np.float32)
+            np.add.at(accum, np.asarray(segs["pixel"], np.int64), rgb)  # sequential, segment order
             out["accum"] = accum
         return out
 

@@ -35,7 +35,8 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
     r = bench.roofline(st, a, WL(), 2.0, None, None)
     items = (640 + 63) // 64 * 4
     # 112 B per queued pair: three SegRec planes, the record carries the power (128 B split layout)
-    alg = 64.0 * (1000 + 3000) + items * 64 * (40 + 12) + 112.0 * 500 + 640 * 12 * (4 + 1)
+    # a node visit reads one 128-B Node4 record (4-wide walk), a staged beam line 64 B
+    alg = 128.0 * 1000 + 64.0 * 3000 + items * 64 * (40 + 12) + 112.0 * 500 + 640 * 12 * (4 + 1)
     # without the PMC passes: the HBM roofline of the requested bytes
     assert r["bound"] == "hbm" and r["hbm"]["requested_bytes_per_launch"] == alg
     a_split = bench.parse(["--split", "4", "--split-records", "1"])
@@ -60,3 +61,20 @@ def test_roofline_fraction_is_achieved_over_peak(bench):
 def test_host_threads_positive(bench):
     n, note = bench.host_threads()
     assert n >= 1 and "affinity" in note
+
+
+def test_late_step_is_the_smallest_radius_iteration(bench):
+    """counters_last_iteration and the CPU sample go to the smallest radius the line times: C2's
+    iteration 15 whenever 16 or more steps are timed (the driver's 20 steps re-time 0-3 after it)."""
+    class WL:
+        def iteration(self, k):
+            return k % 16
+
+    assert bench.late_step(WL(), 20) == 15
+    assert bench.late_step(WL(), 16) == 15
+    assert bench.late_step(WL(), 5) == 4
+
+    class Synthetic:
+        iteration = None
+
+    assert bench.late_step(Synthetic(), 7) == 6

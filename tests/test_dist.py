@@ -1,8 +1,9 @@
 """World-size-2 `gloo` tests of the multi-GPU decompositions on CPU: image tiles (one gather of the
 owned-pixel bands) and packet ranges (one sum-reduce of partial films), beams replicated.  Each rank's
 gather is computed by the oracle here (CPU stand-in for libbre, test infrastructure); the checks are
-that the combined frame equals a single-rank render (bit for bit for tiles, to float summation order
-for packets) and that tiles / packet ranges partition the image / the segments."""
+that the combined frame equals a single-rank render (bit for bit for tiles and for packet-class films,
+to float summation order for the sum-reduce of packet films) and that tiles / packet ranges partition
+the image / the segments."""
 import importlib
 import os
 import socket
@@ -25,7 +26,24 @@ def _free_port():
     return port
 
 
-def _render(rank, world, port, outdir, packets=False):
+def _compose_classes(seg_rgb, pixel, seg_pos, npix, classes=8, block=1):
+    """Host restatement of libbre's packet-class compose (bre_sort.hip k_seg_classes / k_pix_compose,
+    the oracle standing in for the GPU): segment i of the gather order (position seg_pos[i]) is in
+    class ((pos // 64) // block) % classes; per class, each pixel's segments are added in order in
+    float32 and the run is added to the class plane once."""
+    acc = np.zeros((classes * npix, 3), np.float32)
+    runs = {}
+    for i in np.argsort(seg_pos, kind="stable"):
+        key = (int(seg_pos[i] // 64 // block) % classes, int(pixel[i]))
+        r = runs.setdefault(key, np.zeros(3, np.float32))
+        r += seg_rgb[i]
+    for (c, p), r in runs.items():
+        if np.any(r != 0):
+            acc[c * npix + p] += r
+    return acc
+
+
+def _render(rank, world, port, outdir, packets=False, classes=1):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -36,9 +54,10 @@ def _render(rank, world, port, outdir, packets=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    frame = dmod.ShardedFrame(W, H, rank, world, packets=packets)
+    frame = dmod.ShardedFrame(W, H, rank, world, packets=packets, classes=classes)
     beams = synth.fog_beams(NB, seed=12345)  # replicated: same seeds on every rank
     segs = synth.camera_segments(W, H, seed=777, pixels=frame.pixels)
+    idx = np.arange(segs["tmax"].shape[0])
     if packets:  # every rank has every segment and gathers its packets p = rank (mod world)
         bre = importlib.import_module("beam-radiance-estimate-pbrt_amd")
         n = segs["tmax"].shape[0]
@@ -47,10 +66,14 @@ def _render(rank, world, port, outdir, packets=False):
         segs = {k: v[idx] for k, v in segs.items()}
     out = load_oracle().build(beams).gather(segs, R)
     acc = frame.accum.numpy()
-    np.add.at(acc, segs["pixel"], out["seg_rgb"])
+    if classes > 1:
+        acc[:] = _compose_classes(out["seg_rgb"], segs["pixel"], idx, W * H, classes)
+    else:
+        np.add.at(acc, segs["pixel"], out["seg_rgb"])
     frame.reduce_to_root(0)
     if rank == 0:
         np.save(os.path.join(outdir, "frame.npy"), frame.accum.numpy())
+        np.save(os.path.join(outdir, "image.npy"), frame.resolve().numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -109,3 +132,30 @@ def test_packet_shards_partition_segments():
                 assert np.array_equal(np.sort(allseg), np.arange(n)), (n, count, chunk)
     assert bre.shard_segments(1000, 2, 2, 1) == 0 and bre.shard_segments(1000, -1, 2, 1) == 0
     assert bre.shard_segments(1000, 0, 2, 0) == 0 and bre.shard_segments(-5, 0, 2, 1) == 0
+
+
+def _render_classes(rank, world, port, outdir):
+    _render(rank, world, port, outdir, packets=True, classes=8)
+
+
+def test_two_rank_gloo_packet_class_films_equal_single_rank_bitwise(tmp_path, oracle, synth):
+    """Packet-class films (dist.ShardedFrame classes=8, libbre BRE_OPT_FILM_CLASSES): two ranks each
+    compute the class planes of their packets, one gather brings them to the root, and the resolved
+    image is the one-rank image BIT FOR BIT (the sum-reduce of partial films above is not)."""
+    port = _free_port()
+    mp.start_processes(_render_classes, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    planes = np.load(tmp_path / "frame.npy")
+    image = np.load(tmp_path / "image.npy")
+    beams = synth.fog_beams(NB, seed=12345)
+    segs = synth.camera_segments(W, H, seed=777)
+    out = oracle.build(beams).gather(segs, R)
+    ref = _compose_classes(out["seg_rgb"], segs["pixel"], np.arange(segs["tmax"].shape[0]), W * H)
+    assert np.abs(planes).max() > 0
+    assert np.array_equal(planes.view(np.uint32), ref.view(np.uint32))
+    img = ref[: W * H].copy()
+    for c in range(1, 8):
+        img += ref[c * W * H:(c + 1) * W * H]
+    assert np.array_equal(image.view(np.uint32), img.view(np.uint32))
+    # and the image is the film to float summation order
+    full = oracle.build(beams).gather(segs, R, npix=W * H)["accum"]
+    assert np.abs(image - full).max() <= 1e-6 * np.abs(full).max()

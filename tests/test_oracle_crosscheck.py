@@ -102,3 +102,24 @@ def test_multithreaded_gather_equals_serial(oracle, synth):
     b = bvh.gather(segs, 0.01, nthreads=4, chunk=16)
     for k in ("seg_rgb", "cand", "visit", "contrib"):
         assert np.array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("kind", ["camera", "bounce"])
+def test_skip_gather_equals_reference_form(oracle, synth, kind):
+    """The image-parity gather (ora_gather_skip) skips only candidates whose double line distance
+    proves they cannot contribute: its per-segment sums and counts are the reference form's bit for
+    bit, and it does skip (most candidates, at a small radius)."""
+    beams = synth.fog_beams(4000, seed=81)
+    segs = synth.camera_segments(40, 30, seed=82) if kind == "camera" else synth.bounce_segments(1200, seed=83)
+    bvh = oracle.build(beams)
+    for R in (0.002, 0.01, 0.05):
+        ref = bvh.gather(segs, R, nthreads=2)
+        got = bvh.gather_skip(segs, R, npix=int(segs["pixel"].max()) + 1, nthreads=3)
+        assert np.array_equal(ref["seg_rgb"].view(np.uint32), got["seg_rgb"].view(np.uint32))
+        assert np.array_equal(ref["cand"], got["cand"]) and np.array_equal(ref["contrib"], got["contrib"])
+        assert got["skipped"].sum() > 0.5 * (got["cand"].sum() - got["contrib"].sum())
+        # the film: per-segment sums added in segment order
+        acc = np.zeros_like(got["accum"])
+        for s in range(segs["tmax"].shape[0]):
+            acc[segs["pixel"][s]] += got["seg_rgb"][s]
+        assert np.array_equal(acc, got["accum"])

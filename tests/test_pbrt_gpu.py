@@ -123,3 +123,61 @@ def test_big_mesh_pbrt_render_matches_oracle(bre, pb, oracle):
     ref = pb.film_finalize((ld / p.end_iteration).astype(np.float32))
     assert img.mean() > 0
     assert _rel_l2(img.reshape(-1, 3), ref) <= 1e-5
+
+
+C1 = open(os.path.join(SCENES, "cornell_fog_c1.pbrt")).read().replace(
+    'Include "cornell_world.pbrt"', open(os.path.join(SCENES, "cornell_world.pbrt")).read())
+
+
+def _imgtool_diff(a, b):
+    """The reference's `imgtool diff` figures (src/tools/imgtool.cpp:393-432): over the RGB channels
+    where either image is nonzero, relative differences |a - b| / a above 0.5% (small) and 5% (big),
+    and the relative difference of the two images' means."""
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    nz = ~((a == 0) & (b == 0))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = np.abs(a[nz] - b[nz]) / a[nz]
+    avg0, avg1 = a[nz].sum() / a.size, b[nz].sum() / b.size
+    return {"small": int(np.sum(d > 0.005)), "big": int(np.sum(d > 0.05)),
+            "avg_delta_pct": 100.0 * (avg0 - avg1) / min(avg0, avg1), "channels": int(a.size)}
+
+
+def _threads():
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return int(omp) if omp.isdigit() and int(omp) > 0 else min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.mark.parametrize("arith", ["cephes", "libm"])
+def test_c1_full_image_matches_oracle(bre, pb, oracle, arith):
+    """BASELINE configs[0] at its own size: scenes/cornell_fog_c1.pbrt UNMODIFIED (256x256, 50k photons,
+    1 iteration, R0 0.01) rendered by bre_pbrt_render on the GPU, against the oracle chain -- camera pass,
+    photon pass, the reference's SAH tree and gather (every candidate in DFS order; ora_gather_skip),
+    Film::SetImage + WriteImage -- over the whole film.  `cephes`: the oracle with the transcendentals
+    the GPU shares (include/bre_fmath.h); `libm`: with the host libm, the reference's arithmetic.  The
+    north star's bar is 1e-3 relative L2; the imgtool counts are printed beside it."""
+    s = pb.parse_string(C1)
+    assert s.ok, s.messages
+    w, h, p = s.film["xres"], s.film["yres"], s.params
+    assert (w, h, p.end_iteration, p.photons_per_iteration, p.max_depth) == (256, 256, 1, 50000, 5)
+    assert abs(p.initial_radius - 0.01) < 1e-9
+    img = s.render(write_files=False)
+    R = np.float32(bre.beam_radius_at(p.initial_radius, p.alpha, 0))
+    oracle.set_libm(arith == "libm")
+    try:
+        cam = oracle.camera_pass(s.scene, w, h, iteration=0, max_depth=p.max_depth)
+        beams = oracle.trace_photons(s.scene, p.photons_per_iteration, iteration=0, max_depth=p.max_depth, radius=R)
+    finally:
+        oracle.set_libm(False)
+    out = oracle.build(beams).gather_skip({k: cam[k] for k in ("o", "p", "d", "tmax", "pixel")}, R, npix=w * h,
+                                          nthreads=_threads())
+    ref = pb.film_finalize((cam["surface"].astype(np.float32) + out["accum"]).astype(np.float32))
+    l2 = _rel_l2(img.reshape(-1, 3), ref)
+    diff = _imgtool_diff(img.reshape(-1, 3), ref)
+    print(f"C1 full film ({arith} oracle): rel-L2 {l2:.3e}, imgtool {diff}, segments {cam['tmax'].shape[0]}, "
+          f"beams {beams['radius'].shape[0]}, candidates {int(out['cand'].sum())}, "
+          f"contributions {int(out['contrib'].sum())}")
+    assert img.mean() > 0
+    assert l2 <= 1e-3
+    if arith == "cephes":  # the same arithmetic as the GPU: only float summation order differs
+        assert l2 <= 1e-5

@@ -89,3 +89,57 @@ def test_packet_shards_sum_to_single_render(bre, scene_mod_gpu, world, chunk):
     assert _rel_l2(got, want) <= 1e-6
     big = want.max(axis=1) > 1e-3 * want.max()
     assert (np.abs(got - want)[big] <= 1e-4 * np.abs(want[big]).max(axis=1, keepdims=True)).all()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_packet_class_films_equal_single_render_bitwise(bre, scene_mod_gpu, world):
+    """Packet-class films (BRE_OPT_FILM_CLASSES 8, dist.ShardedFrame classes=8; the bench's default):
+    over three iterations each packet shard computes the class planes c = rank (mod N) of its packets,
+    and they are the one-GPU planes BIT FOR BIT; the planes a rank does not own stay zero; the planes
+    gathered to the root (what gather_to_root does over RCCL) resolve to the one-GPU image bit for
+    bit, and bre_resolve_classes gives the same bits as the frame's resolve.  The partial-film
+    reduce above matches only to float summation order."""
+    import torch
+
+    dmod = importlib.import_module("beam-radiance-estimate-pbrt_amd.dist")
+    W, H = 256, 192
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+
+    def render(rank, count, frame):
+        with bre.BeamGather(0) as g:
+            g.set_stream(torch.cuda.current_stream().cuda_stream)  # the torch adds in stream order
+            g.set_film_classes(bre.FILM_CLASSES)
+            if count > 1:
+                g.set_shard(rank, count, 1, packets=True)
+            for it in range(3):
+                R = bre.beam_radius_at(0.01, 0.5, it)
+                ld = torch.zeros_like(frame.accum)
+                g.trace_photons(scene, 150_000, it, 5, R)
+                g.camera_pass(scene, W, H, it, 5, True, True, surface=ld)
+                g.gather_camera(R, ld)
+                frame.accum.add_(ld)
+            g.synchronize()
+            img = torch.zeros((W * H, 3), dtype=torch.float32, device="cuda")
+            g.resolve_classes(frame.accum, img)
+            g.synchronize()
+        return img
+
+    ref = dmod.ShardedFrame(W, H, 0, 1, device="cuda", packets=True, classes=8)
+    img_lib = render(0, 1, ref)
+    want = ref.resolve()
+    assert torch.equal(img_lib, want)  # bre_resolve_classes == the frame's resolve, bit for bit
+    assert float(want.abs().max()) > 0
+    frames = [dmod.ShardedFrame(W, H, r, world, device="cuda", packets=True, classes=8) for r in range(world)]
+    for r, f in enumerate(frames):
+        render(r, world, f)
+        for c in range(8):
+            if c % world == r:
+                assert torch.equal(f.plane(c), ref.plane(c)), (r, c)
+            else:
+                assert not bool(f.plane(c).any()), (r, c)
+    root = frames[0]
+    for r, f in enumerate(frames[1:], 1):  # the gather of the owned planes
+        for c in f.owned_planes():
+            root.plane(c).copy_(f.plane(c))
+    got = root.resolve()
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))
