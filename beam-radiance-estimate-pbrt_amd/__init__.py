@@ -192,12 +192,17 @@ class BeamGather:
             self.set_option(OPT_PREFILTER, int(prefilter))
         self._keep = []
 
+    _classes = 1  # BRE_OPT_FILM_CLASSES as set through this wrapper
+    _cam_npix = 0  # pixels of the last camera pass
+
     def _check(self, st):
         if st != BRE_OK:
             raise BreError(st, self.lib.bre_last_error(self.h).decode())
 
     def set_option(self, opt: int, value: int):
         self._check(self.lib.bre_set_option(self.h, opt, int(value)))
+        if opt == OPT_FILM_CLASSES:
+            self._classes = int(value)
 
     def set_shard(self, rank: int, count: int, block: int = 1, packets: bool = False, roots: bool = False):
         """Tile shards (default): the camera pass walks only the 16x16 image tiles of the blocks of
@@ -215,6 +220,18 @@ class BeamGather:
     def set_film_classes(self, classes: int):
         """BRE_OPT_FILM_CLASSES: 1 (one film) or FILM_CLASSES (8 planes per film, see include/bre.h)."""
         self.set_option(OPT_FILM_CLASSES, int(classes))
+
+    def _film(self, buf, npix: int, what: str):
+        """A caller film must hold classes * 3 * npix floats: the library writes plane p % classes of
+        pixel p through a raw pointer, so a short buffer is refused here, before any launch."""
+        if buf is None:
+            return None
+        need = self._classes * 3 * int(npix)
+        n = buf.numel() if hasattr(buf, "numel") else int(np.asarray(buf).size)
+        if n < need:
+            raise ValueError(f"{what}: film of {n} floats, the context's {self._classes} film class(es) over "
+                             f"{npix} pixels need {need}")
+        return buf
 
     def resolve_classes(self, classes, out):
         """out (npix, 3) = the sum of the 8 class planes of `classes` ((8 * npix, 3) or (8, npix, 3),
@@ -277,18 +294,22 @@ class BeamGather:
         """Camera pass on the GPU (photonbeam.cpp:444-555).  `surface`: optional torch float32
         CUDA tensor (W*H, 3) receiving += the surface radiance.  Returns the segment count."""
         n = ctypes.c_int64(0)
+        self._film(surface, int(width) * int(height), "camera_pass surface")
         self._check(self.lib.bre_camera_pass(self.h, ctypes.addressof(scene), int(width), int(height),
                                              int(iteration), int(max_depth), int(render_surfaces),
                                              int(render_media), _ptr(surface), ctypes.byref(n)))
+        self._cam_npix = int(width) * int(height)
         return n.value
 
     def gather_camera(self, R: float, accum):
         """Gather the last camera pass's segments into `accum` (torch CUDA tensor (W*H, 3))."""
+        self._film(accum, self._cam_npix, "gather_camera accum")
         self._check(self.lib.bre_gather_camera(self.h, float(R), _ptr(accum)))
 
     def gather_camera_segments(self, R: float, accum=None, seg_rgb=None, counts=None):
         """bre_gather_camera with per-segment outputs (torch CUDA tensors, camera-pass order):
         seg_rgb (n, 3) float32, counts (n, 2) int32 ({C or -1, contributions})."""
+        self._film(accum, self._cam_npix, "gather_camera_segments accum")
         self._check(self.lib.bre_gather_camera_segments(self.h, float(R), _ptr(accum), _ptr(seg_rgb), _ptr(counts)))
 
     def get_segments(self):
@@ -304,6 +325,7 @@ class BeamGather:
 
     # ---- the integrator ----
     def render_iteration(self, scene, params, iteration: int, ld):
+        self._film(ld, int(params.width) * int(params.height), "render_iteration ld")
         self._check(self.lib.bre_render_iteration(self.h, ctypes.addressof(scene), ctypes.addressof(params),
                                                   int(iteration), _ptr(ld)))
 
@@ -336,6 +358,7 @@ class BeamGather:
     def gather_device(self, o, p, d, tmax, pixel, R, npix, accum=None, seg_rgb=None, counts=None):
         """Device tensors; asynchronous on the context stream."""
         n = tmax.shape[0]
+        self._film(accum, npix, "gather_device accum")
         self._check(self.lib.bre_gather_device(self.h, n, _ptr(o), _ptr(p), _ptr(d), _ptr(tmax), _ptr(pixel),
                                                float(R), int(npix), _ptr(accum), _ptr(seg_rgb), _ptr(counts)))
 

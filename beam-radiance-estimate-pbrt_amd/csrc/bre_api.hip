@@ -1414,6 +1414,7 @@ bre_status bre_render_progressive(bre_ctx *c, const bre_scene *scene, const bre_
     if (!c) return BRE_ERR_INVALID_ARG;
     bre_status st = check_params(c, rp);
     if (st != BRE_OK) return st;
+    if (c->film_classes > 1) return fail(c, BRE_ERR_STATE, "bre_render*: BRE_OPT_FILM_CLASSES is for caller device films");
     st = set_device(c);
     if (st != BRE_OK) return st;
     const int64_t npix = (int64_t)rp->width * rp->height;
@@ -1466,6 +1467,7 @@ bre_status bre_render(bre_ctx *c, const bre_scene *scene, const bre_render_param
     if (!c) return BRE_ERR_INVALID_ARG;
     bre_status st = check_params(c, rp);
     if (st != BRE_OK) return st;
+    if (c->film_classes > 1) return fail(c, BRE_ERR_STATE, "bre_render: BRE_OPT_FILM_CLASSES is for caller device films");
     if (!image) return fail(c, BRE_ERR_INVALID_ARG, "bre_render: null image");
     FinalImage f{image, (size_t)rp->width * rp->height * 3};
     if (rp->end_iteration == rp->start_iteration) {
@@ -1585,6 +1587,8 @@ bre_status bre_gather(bre_ctx *c, int64_t nseg, const float *o, const float *p, 
                       int32_t *seg_counts) {
     if (!c) return BRE_ERR_INVALID_ARG;
     if (nseg < 0 || npix < 0) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: negative size");
+    if (c->film_classes > 1 && accum)
+        return fail(c, BRE_ERR_STATE, "bre_gather: BRE_OPT_FILM_CLASSES is for caller device films (bre_gather_device)");
     if (nseg > 0 && (!o || !p || !d || !tmax))
         return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: null segment array");
     if (accum && !pixel) return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: accum_rgb given without seg_pixel");
@@ -1687,6 +1691,9 @@ bre_status bre_gather_sharded(bre_ctx *const *ctxs, int n_ctx, int64_t nseg, con
     bre_status st = check_ctxs(ctxs, n_ctx);
     if (st != BRE_OK) return st;
     if (nseg < 0 || npix < 0) return fail(ctxs[0], BRE_ERR_INVALID_ARG, "bre_gather_sharded: negative size");
+    for (int i = 0; i < n_ctx; ++i)
+        if (ctxs[i]->film_classes > 1)
+            return fail(ctxs[0], BRE_ERR_STATE, "bre_gather_sharded: BRE_OPT_FILM_CLASSES is for caller device films");
     const size_t F = accum && npix > 0 ? (size_t)npix * 3 : 0, S = (size_t)nseg;
     // per context: its partial film and per-segment outputs (only its own packets' entries are
     // nonzero); the contexts' shard options are set for the call and restored afterwards

@@ -136,12 +136,12 @@ hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s
 // arbitrary lanes of the packet touches at most 1 KB (16 lines) instead of 64 separate lines.
 struct alignas(16) SegRec {
     float o[3], tmax;   // ray.o, ray.tMax
-    float p[3], mag_a;  // isect.p, |p - o|
+    float p[3], mag_a;  // isect.p, |p - o|, negated (sign bit set) when some 1 / d_i is infinite
     float au[3];        // (p - o) * (1 / |p - o|)
     int32_t has_inf;    // some 1 / d_i is infinite (axis-parallel ray)
     float invs[3];      // 1 / d with infinities replaced by +-FLT_MAX
-    int32_t has_inf3;   // has_inf again: the tile kernel's exact stage reads planes 0, 1 and 3 and
-                        // recomputes au from o, p and |A| (BRE_AU_RECOMPUTE)
+    float inv_mag_a;    // RN(1 / |p - o|) (0 for a zero-length segment): the tile kernel's exact stage
+                        // reads planes 0, 1 and 3 and recomputes au = (p - o) * inv_mag_a
 };
 static_assert(sizeof(SegRec) == 64, "SegRec must be one 64-B line");
 // plane k (0..3) of segment s in the packet-plane layout (buffers hold ceil(nseg / 64) * 64 records)

@@ -64,14 +64,11 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_SQRT_NOSCALE
 #define BRE_SQRT_NOSCALE 1
 #endif
-// BRE_BUNDLE_LINE 1: the packet bundle line through the centres of the lanes' origin and end-point
-// boxes instead of the mean origin and mean direction (A/B)
-#ifndef BRE_BUNDLE_LINE
-#define BRE_BUNDLE_LINE 0
-#endif
-// BRE_AXIS_BOX 1: the tile axis (k_tile_axis) through the centres of the beams' start and end boxes (A/B)
-#ifndef BRE_AXIS_BOX
-#define BRE_AXIS_BOX 0
+// BRE_DIR_SPREAD 1: the packet line reject bounds the lanes' spread along the common normal of the
+// bundle line and the beam (an octagon of directional extents, make_bundle) instead of by the bundle's
+// radius (A/B)
+#ifndef BRE_DIR_SPREAD
+#define BRE_DIR_SPREAD 1
 #endif
 // The exact stage reads the SegRec planes through a buffer descriptor (SGPR base + 32-bit lane offset:
 // one VALU of address arithmetic instead of 64-bit pointer math; with the power too, C2 +0.8%, C3 +2%,
@@ -221,7 +218,6 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
     K.omax = wave_max(valid ? L.omax : 0.f);
     bool ok = cnt > 0 && sl > 0.f && isfinite(sl);
     K.cu = ok ? mk(su.x / sl, su.y / sl, su.z / sl) : mk(0.f, 0.f, 1.f);
-#if BRE_BUNDLE_LINE
     {
         // the line through the centres of the origins' and the end points' boxes: closer to the
         // minimax line than the mean line when the lanes' lengths differ (any line is valid: delta is
@@ -240,7 +236,6 @@ __device__ __forceinline__ Bundle make_bundle(const Lane &L, bool valid) {
             ok = true;
         }
     }
-#endif
     const auto perp = [&](f3 x) {
         const f3 t = sub3(x, K.co);
         const f3 c = mk(t.y * K.cu.z - t.z * K.cu.y, t.z * K.cu.x - t.x * K.cu.z, t.x * K.cu.y - t.y * K.cu.x);
@@ -470,18 +465,14 @@ __global__ __launch_bounds__(64) void k_tile_axis(const BeamRec *__restrict__ re
         return;
     }
     const f3 e = add3(b0, scale3(bu, mb));
-#if BRE_AXIS_BOX
-    // the axis through the centres of the starts' and the ends' boxes (A/B against the means)
+    // the axis through the centres of the starts' and the ends' boxes (round 5: C2 +1.2% over the
+    // mean start -> mean end, profiles/r5/run3)
     const auto ctr = [&](float v) {
         const float hi = wave_max(ok ? v : -FLT_MAX), lo = -wave_max(ok ? -v : -FLT_MAX);
         return 0.5f * lo + 0.5f * hi;
     };
     const f3 ps = mk(ctr(b0.x), ctr(b0.y), ctr(b0.z));
     const f3 pe = mk(ctr(e.x), ctr(e.y), ctr(e.z));
-#else
-    const f3 ps = mk(wave_sum(ok ? b0.x : 0.f) / n, wave_sum(ok ? b0.y : 0.f) / n, wave_sum(ok ? b0.z : 0.f) / n);
-    const f3 pe = mk(wave_sum(ok ? e.x : 0.f) / n, wave_sum(ok ? e.y : 0.f) / n, wave_sum(ok ? e.z : 0.f) / n);
-#endif
     f3 d = sub3(pe, ps);
     const float dl = sqrtf(lensq3(d));
     d = (dl > 1e-6f * (1.f + fabsf(ps.x) + fabsf(ps.y) + fabsf(ps.z)) && isfinite(dl)) ? scale3(d, 1.f / dl)
@@ -728,12 +719,14 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const __amdgpu_buffer_rsrc_t srs = buf_rsrc(srec);
     const unsigned int so_ = (unsigned int)(seg0 >> 6) << 12, vo = (unsigned int)sl << 4;
     const float4 s0 = buf_f4(srs, vo, so_), s3 = buf_f4(srs, vo + 3072u, so_), bx = rb[0], by = rb[1];
-    // au = (p - o) * (1 / |A|) by load_lane's own operations (bit-identical to plane 2, which is not
-    // loaded): VALU, which has headroom, for one of the pair's eight vector loads (the texture-data
-    // path is the kernel's busiest unit); has_inf from plane 3
+    // au = (p - o) * RN(1 / |A|), load_lane's own operations with the reciprocal k_seg_prep stored in
+    // plane 3 (bit-identical to plane 2, which is not loaded: VALU for one of the pair's eight vector
+    // loads -- the texture-data path is the kernel's busiest unit -- without a division per pair).
+    // Plane 1's w is |A| with the sign bit carrying has_inf.
     const float4 s1 = buf_f4(srs, vo + 1024u, so_), bz = rb[2], bw = rb[3];
-    const f3 au_ = (s1.w != 0.0f) ? div3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s1.w) : mk(0.f, 0.f, 0.f);
-    const float4 s2 = make_float4(au_.x, au_.y, au_.z, s3.w);
+    const float mag_a = fabsf(s1.w);
+    const f3 au_ = (mag_a != 0.0f) ? scale3(sub3(mk(s1.x, s1.y, s1.z), mk(s0.x, s0.y, s0.z)), s3.w) : mk(0.f, 0.f, 0.f);
+    const float4 s2 = make_float4(au_.x, au_.y, au_.z, 0.f);
     // a uniform-radius set's power is in the record's last three words (BeamRec): seven loads per pair
     const float4 pv = bset.uniform ? make_float4(bw.y, bw.z, bw.w, 0.f) : pw[b];
     // phase 1: the box test (segment o, tmax, 1/d; the beam's box)
@@ -742,7 +735,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     const Box6 box{bx.x, bx.y, bx.z, bx.w, by.x, by.y};
     float te;
     bool hit = on & node_test(box, o, mk(s3.x, s3.y, s3.z), tmax, te);
-    const bool inf = s2.w != 0.f;  // has_inf (integer 1 as float bits: a denormal, never 0)
+    const bool inf = __builtin_signbit(s1.w) != 0;  // has_inf, the sign of plane 1's |A|
     if (__ballot(on & inf) != 0ull) {
         if (on & inf) {
             // the rare axis-parallel ray: the literal slab test on its exact 1/d
@@ -759,7 +752,7 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     if (hit) {
         const float maxd = R + beam_radius(bset, bw.y);  // MaxDistance = currentBeamRadius + beam->radius
         float d2, unused;
-        const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), s1.w,
+        const bool ok = closest_distance_t<false, true>(o, mk(s1.x, s1.y, s1.z), mk(s2.x, s2.y, s2.z), mag_a,
                                                         mk(by.z, by.w, bz.x), mk(bz.y, bz.z, bz.w), bw.x, d2, unused);
         // |pA - pB| correctly rounded (photonbeam.cpp:500).  Without the compiler's small-input scaling
         // when maxd >= 2^-30: for d2 >= 2^-96 the root is bit-identical; below, both roots are < 2^-47.9,
@@ -1258,9 +1251,11 @@ __global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__r
     load_lane(s, nseg, so, sp_, sd, stmax, L);
     float4 *q = const_cast<float4 *>(seg_plane(out, s, 0));  // packet-plane layout (bre_device.h)
     q[0] = make_float4(L.o.x, L.o.y, L.o.z, L.tmax);
-    q[64] = make_float4(L.p.x, L.p.y, L.p.z, L.mag_a);
+    // |A| >= 0: its sign bit carries has_inf; plane 3's w is RN(1 / |A|) (0 for a zero-length segment),
+    // the reciprocal div3 forms in load_lane, so the exact stage recomputes au without a division
+    q[64] = make_float4(L.p.x, L.p.y, L.p.z, L.has_inf ? -L.mag_a : L.mag_a);
     q[128] = make_float4(L.au.x, L.au.y, L.au.z, __int_as_float(L.has_inf ? 1 : 0));
-    q[192] = make_float4(L.invs.x, L.invs.y, L.invs.z, __int_as_float(L.has_inf ? 1 : 0));
+    q[192] = make_float4(L.invs.x, L.invs.y, L.invs.z, L.mag_a != 0.0f ? 1.0f / L.mag_a : 0.0f);
 }
 
 // Sum the per-subtree partials of each segment in subtree order; write seg_rgb and add the

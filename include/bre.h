@@ -111,7 +111,12 @@ typedef enum bre_option {
                                 of the planes in class order (bre_resolve_classes).  Packet shard r of
                                 count (count dividing 8) computes exactly classes c % count == r, so
                                 gathering the shards' planes and resolving gives the 1-shard image
-                                bit for bit (dist.py ShardedFrame, bench.py --gpus N). */
+                                bit for bit (dist.py ShardedFrame, bench.py --gpus N).  The caller's
+                                film buffers (bre_camera_pass d_surface, bre_gather_camera*,
+                                bre_gather_device, bre_render_iteration) must then hold 8 * 3 * npix
+                                floats; the entry points with films of their own (bre_gather,
+                                bre_render, bre_render_progressive, bre_gather_sharded) refuse the
+                                option with BRE_ERR_STATE. */
 } bre_option;
 
 #define BRE_FILM_CLASSES 8

@@ -14,7 +14,8 @@ trap 'kill $TICK' EXIT
 # refusals / XCD map fallback / empty packet shard, the full-size C1 image against the oracle chain
 timeout -k 10 900 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread \
     tests/test_shard_gpu.py tests/test_root_shards_gpu.py tests/test_pipeline_gpu.py \
-    tests/test_film_determinism_gpu.py tests/test_pbrt_gpu.py > "$OUT/pytest.log" 2>&1 \
+    tests/test_film_determinism_gpu.py tests/test_pbrt_gpu.py tests/test_c2_production.py tests/test_gpu_parity.py \
+    tests/test_prefilter_options_gpu.py > "$OUT/pytest.log" 2>&1 \
     || { echo "pytest failed"; tail -n 60 "$OUT/pytest.log"; exit 1; }
 tail -n 1 "$OUT/pytest.log"
 grep -E "^C1 full film" "$OUT/pytest.log"

@@ -62,3 +62,19 @@ def test_null_and_no_device_paths_fail_cleanly(bre):
         assert st == 5 and not h.value  # BRE_ERR_NO_DEVICE, no context
         with pytest.raises(bre.BreError):
             bre.BeamGather(0)
+
+
+def test_film_buffers_are_checked_against_the_film_classes(bre):
+    """With BRE_OPT_FILM_CLASSES the library writes 8 planes of 3 * npix floats through the caller's raw
+    film pointer; the Python wrapper refuses a shorter buffer before any launch (a one-plane film
+    under an 8-class context was an out-of-bounds write in the round-5 bench refactor)."""
+    class Ctx:
+        _classes = bre.FILM_CLASSES
+
+    film = np.zeros((8 * 100, 3), np.float32)
+    assert bre.BeamGather._film(Ctx(), film, 100, "t") is film
+    with pytest.raises(ValueError):
+        bre.BeamGather._film(Ctx(), np.zeros((100, 3), np.float32), 100, "t")
+    Ctx._classes = 1
+    assert bre.BeamGather._film(Ctx(), np.zeros((100, 3), np.float32), 100, "t") is not None
+    assert bre.BeamGather._film(Ctx(), None, 100, "t") is None
