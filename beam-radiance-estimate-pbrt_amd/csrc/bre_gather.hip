@@ -1324,75 +1324,127 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
 // waves on the largest subtrees are dispatched first and the kernel's tail is made of small ones.
 // The leaves below a Karras node are a contiguous range (bre_build.hip), found by its leftmost and
 // rightmost descents.  The partial sums are added in this root order (k_reduce): deterministic.
+//
+// Starting from the root, the frontier's LARGEST internal node (leaf tiles below it, Node::nleaf; ties:
+// the lowest frontier position) is replaced by its children (the first in its place, the second
+// appended) while the frontier stays within S entries, so the S work roots are as equal in size as
+// the tree allows: the longest (packet, subtree) waves, which end the launch, are as short as they can
+// be (a breadth-first frontier left subtrees of very unequal size, and an emulated 1/8 rank's
+// iteration-0 gather 37% above 1/8 of N = 1's).  Then the roots are ordered largest first (ties in
+// frontier order) for the LPT block map.
+//
+// The greedy loop is serial (up to S - 1 expansions: 0.39 ms at C2 as a block-wide reduction per
+// expansion), but its result is not: every expanded node has more leaf tiles than its children, so
+// the expansions come in decreasing order of size and the expanded set E is the S - 1 largest
+// interior nodes (fewer when the tree has fewer), a subtree from the root; the roots are E's children
+// outside E.  So, with all threads:
+//   1. cache, breadth first, every interior node with at least total / S leaf tiles (the frontier
+//      partitions the total over <= S entries, so its largest entry, the only one ever expanded, has
+//      at least total / S): its leaf tiles, children, their leaf tiles and cache slots;
+//   2. E = the S - 1 cached nodes of largest (leaf tiles, -index), each ranked against all others;
+//   3. the roots: E's children outside E (the whole tree's root when S = 1);
+//   4. ranks: leaf tiles descending, ties by child index.
+// Ties of equal size are broken by node index instead of the frontier position the serial form used
+// (any frontier is a valid split; this one is deterministic).  A cache overflow (never seen: C2 caches
+// ~600 of 4096 slots at S = 256) still yields a valid split: the cached nodes form a subtree from the
+// root, so E's top-(S - 1) choice among them is one too.
+constexpr int kRootSlots = 4096;
+struct RootsShared {
+    int32_t id[kRootSlots];     // cached node
+    int32_t nl[kRootSlots];     // its leaf tiles (Node::nleaf)
+    int32_t ch[kRootSlots][2];  // its children
+    int32_t cw[kRootSlots][2];  // their leaf tiles (1: a leaf tile, 0: empty)
+    int32_t cs[kRootSlots][2];  // their cache slots (-1: not cached)
+    unsigned char in_e[kRootSlots];
+    int32_t fc[kMaxSplit + 1], fw[kMaxSplit + 1];  // the roots, unordered
+    int cnt, lo, hi, nf;
+};
+
+// children, parent and leaf tiles of node x: the record's last 16 bytes
+__device__ __forceinline__ int4 node_tail(const Node *__restrict__ nodes, int32_t x) {
+    return *reinterpret_cast<const int4 *>(&nodes[x].child[0]);
+}
+
 __global__ __launch_bounds__(kMaxSplit) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    // One block, one frontier entry per thread (S <= kMaxSplit = blockDim).  Starting from the
-    // root, the frontier's LARGEST internal node (leaf tiles below it, Node::nleaf; ties: the lowest
-    // frontier position) is replaced by its children while the frontier stays within S entries, so
-    // the S work roots are as equal in size as the tree allows: the longest (packet, subtree) waves,
-    // which end the launch, are as short as they can be (a breadth-first frontier left subtrees of
-    // very unequal size, and an emulated 1/8 rank's iteration-0 gather 37% above 1/8 of N = 1's).
-    // Then the roots are ordered largest first (ties in frontier order) for the LPT block map.
-    __shared__ int32_t cur[kMaxSplit], wt[kMaxSplit];
-    __shared__ unsigned long long red[kMaxSplit / 64];
-    __shared__ int n_sh, stop_sh;
+    __shared__ RootsShared sh;
     if (blockIdx.x != 0) return;
     const int t = threadIdx.x;
-    const auto leaves = [&](int32_t c) -> int32_t { return c >= 0 ? nodes[c].nleaf : 1; };
+    const int32_t total = nodes[0].nleaf;
+    const int32_t heavy = total / S;
     if (t == 0) {
-        cur[0] = 0;
-        wt[0] = leaves(0);
-        n_sh = 1;
+        sh.id[0] = 0;
+        sh.cnt = 1;
+        sh.lo = 0;
+        sh.hi = 1;
+        sh.nf = 0;
     }
     __syncthreads();
+    // 1. breadth-first cache of the heavy interior nodes
     while (true) {
-        const int n = n_sh;
-        // the largest internal entry: key = (leaves << 32) | ~position, maximised over the block
-        unsigned long long key = 0ull;
-        if (t < n && cur[t] >= 0) key = ((unsigned long long)(unsigned int)wt[t] << 32) | (0xffffffffu - (unsigned int)t);
+        const int a = sh.lo, b = sh.hi;
+        if (a >= b) break;
+        for (int k = a + t; k < b; k += kMaxSplit) {
+            const int4 q = node_tail(nodes, sh.id[k]);
+            sh.nl[k] = q.w;
+            const int32_t c[2] = {q.x, q.y};
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const unsigned int lo = (unsigned int)__shfl_xor((int)(unsigned int)key, off);
-            const unsigned int hi = (unsigned int)__shfl_xor((int)(unsigned int)(key >> 32), off);
-            const unsigned long long o = ((unsigned long long)hi << 32) | lo;
-            key = o > key ? o : key;
+            for (int j = 0; j < 2; ++j) {
+                const int32_t w = c[j] == kEmptyChild ? 0 : (c[j] < 0 ? 1 : node_tail(nodes, c[j]).w);
+                int32_t s = -1;
+                if (c[j] >= 0 && w >= heavy) {
+                    s = atomicAdd(&sh.cnt, 1);
+                    if (s < kRootSlots) sh.id[s] = c[j];
+                    else s = -1;
+                }
+                sh.ch[k][j] = c[j];
+                sh.cw[k][j] = w;
+                sh.cs[k][j] = s;
+            }
         }
-        if ((t & 63) == 0) red[t >> 6] = key;
         __syncthreads();
         if (t == 0) {
-            unsigned long long k = red[0];
-            for (int j = 1; j < kMaxSplit / 64; ++j) k = red[j] > k ? red[j] : k;
-            int stop = 1;
-            if (k != 0ull) {
-                const int i = (int)(0xffffffffu - (unsigned int)k);
-                const Node &nd = nodes[cur[i]];
-                const int32_t c0 = nd.child[0], c1 = nd.child[1];
-                const int add = (c0 != kEmptyChild) + (c1 != kEmptyChild) - 1;
-                if (n + add <= S) {
-                    stop = 0;
-                    const int32_t first = c0 != kEmptyChild ? c0 : c1;
-                    cur[i] = first;
-                    wt[i] = leaves(first);
-                    if (add == 1) {
-                        cur[n] = c1;
-                        wt[n] = leaves(c1);
-                    }
-                    n_sh = n + add;
-                }
-            }
-            stop_sh = stop;
+            sh.lo = b;
+            sh.hi = min(sh.cnt, kRootSlots);
         }
         __syncthreads();
-        if (stop_sh) break;
     }
-    const int n = n_sh;
-    const int32_t r = t < n ? cur[t] : 0, w = t < n ? wt[t] : 0;
-    if (t < n) {
-        int rank = 0;  // leaves descending, ties in frontier order
-        for (int j = 0; j < n; ++j) {
-            const int32_t v = wt[j];
-            rank += (v > w) | ((v == w) & (j < t));
+    const int nc = min(sh.cnt, kRootSlots);
+    const auto key = [](int32_t w, int32_t x) -> unsigned long long {
+        return ((unsigned long long)(unsigned int)w << 32) | (0xffffffffu - ((unsigned int)x ^ 0x80000000u));
+    };
+    // 2. E: the S - 1 largest cached nodes
+    for (int k = t; k < nc; k += kMaxSplit) {
+        const unsigned long long kk = key(sh.nl[k], sh.id[k]);
+        int rank = 0;
+        for (int j = 0; j < nc; ++j) rank += key(sh.nl[j], sh.id[j]) > kk;
+        sh.in_e[k] = rank < S - 1;
+    }
+    __syncthreads();
+    // 3. the roots: E's children outside E
+    for (int k = t; k < nc; k += kMaxSplit) {
+        if (!sh.in_e[k]) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int32_t c = sh.ch[k][j], s = sh.cs[k][j];
+            if (c == kEmptyChild || (s >= 0 && sh.in_e[s])) continue;
+            const int f = atomicAdd(&sh.nf, 1);
+            sh.fc[f] = c;
+            sh.fw[f] = sh.cw[k][j];
         }
-        roots[rank] = r;
+    }
+    if (t == 0 && !sh.in_e[0]) {  // S = 1: the whole tree
+        sh.fc[0] = 0;
+        sh.fw[0] = total;
+        sh.nf = 1;
+    }
+    __syncthreads();
+    // 4. ranks: leaf tiles descending, ties by child index
+    const int n = sh.nf;
+    if (t < n) {
+        const unsigned long long kk = key(sh.fw[t], sh.fc[t]);
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += key(sh.fw[j], sh.fc[j]) > kk;
+        roots[rank] = sh.fc[t];
     }
     if (t >= n && t < S) roots[t] = kEmptyChild;
     if (t == 0) roots[S] = n;

@@ -99,6 +99,7 @@ def parse(argv=None):
     ap.add_argument("--film-compose", type=int, default=-1, help=argparse.SUPPRESS)  # film accumulation A/B (option 114)
     ap.add_argument("--photon-single", type=int, default=-1, help=argparse.SUPPRESS)  # photon pass form A/B (option 116)
     ap.add_argument("--pass-priority", type=int, default=-1, help=argparse.SUPPRESS)  # option 117 A/B
+    ap.add_argument("--partial-mib", type=int, default=-1, help=argparse.SUPPRESS)  # option 109: launches per gather
     ap.add_argument("--film-classes", type=int, default=1,
                     help="packet shards: keep the film as 8 packet-class planes, gathered and resolved in class "
                          "order, so every N dividing 8 renders the one-GPU film bit for bit (0: one film, "
@@ -450,7 +451,8 @@ def make_context(bre, args, dev):
     for opt, val in ((102, args.occupancy if args.occupancy else -1), (bre.OPT_TILE_LEAF, args.tile_leaf or -1),
                      (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
                      (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose),
-                     (116, args.photon_single), (117, args.pass_priority)):
+                     (116, args.photon_single), (117, args.pass_priority),
+                     (109, args.partial_mib)):
         if val >= 0:
             c.set_option(opt, val)
     if film_classes(args) > 1:

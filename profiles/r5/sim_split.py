@@ -60,7 +60,7 @@ def cost(on, kept):  # the kernel's choice: transposed scan when on * 8 < kept *
     return on if on * 8 < kept * 6 else (kept + 1) // 2
 
 
-GS = (1, 2, 4)
+GS = (1, 2, 4, 8)
 t0 = time.time()
 for pi in pk:
     sl = slice(pi * 64, pi * 64 + 64)
@@ -96,6 +96,8 @@ for pi in pk:
             else:  # split steps (beam-major, one beam per group per step, two per step for ILP)
                 steps = min(cost(on, int(kall.sum())), (max(ks) + 1) // 2)
             add((kind, f"steps{G}"), steps)
+            add((kind, f"union{G}"), int(kall.sum()) if G > 1 else ks[0])
+            add((kind, f"ustep{G}"), cost(on, int(kall.sum()) if G > 1 else ks[0]))
             add((kind, f"kept{G}"), sum(ks))
 print("it", it, "R %.5f" % R, "packets", npk, "time %.1f s" % (time.time() - t0))
 for kind in ("primary", "bounce"):
@@ -103,5 +105,6 @@ for kind in ("primary", "bounce"):
     if not n:
         continue
     print(f"{kind}: tiles {n}, useful lane pairs/tile {tot[(kind, 'useful')] / n:.1f};",
-          "  ".join(f"G{G}: steps/tile {tot[(kind, f'steps{G}')] / n:.2f} kept/tile {tot[(kind, f'kept{G}')] / n:.1f}"
+          "  ".join(f"G{G}: steps/tile {tot[(kind, f'steps{G}')] / n:.2f} kept/tile {tot[(kind, f'kept{G}')] / n:.1f} "
+                    f"union/tile {tot[(kind, f'union{G}')] / n:.1f} union steps/tile {tot[(kind, f'ustep{G}')] / n:.2f}"
                     for G in GS))
