@@ -240,8 +240,16 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.sort_tmp_bytes = c->sort_tmp.cap;
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_prep(b, c->stream));
-    HIPCHK(c, launch_morton(b, c->stream));
-    HIPCHK(c, launch_sort(b, c->stream));
+    // tree keys 1 / 2 (the tile kernel's tree): the first sort only groups equal centroids (a hash key,
+    // bre_build.hip k_cent_hash); otherwise the centroid Morton order is the tree order
+    const bool se_tree = c->kernel == 0 && c->beam_key >= 1;
+    if (se_tree) {
+        HIPCHK(c, launch_cent_hash(b, c->stream));
+        HIPCHK(c, launch_sort(b, c->stream, 32));
+    } else {
+        HIPCHK(c, launch_morton(b, c->stream));
+        HIPCHK(c, launch_sort(b, c->stream));
+    }
     unsigned int nv[3] = {0u, 0u, 0u};  // valid beams, min / max of their radius bits (k_prep)
     HIPCHK(c, hipMemcpyAsync(nv, b.nvalid, sizeof(nv), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -254,7 +262,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.uniform_radius = c->bset.uniform;
     c->stats.n_beams_valid = nvalid;
     if (nvalid == 0) return BRE_OK;
-    if (c->kernel == 0 && c->beam_key >= 1) {
+    if (se_tree) {
         // tree order by (start, end): group boxes from the centroid order, then the second sort
         HIPCHK(c, c->gbox.ensure(N * 6 * sizeof(float)));
         b.gbox = c->gbox.as<float>();

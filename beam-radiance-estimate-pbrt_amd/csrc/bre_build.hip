@@ -198,6 +198,39 @@ __global__ __launch_bounds__(kBlock) void k_morton(const float *__restrict__ box
     vals[i] = (int32_t)i;
 }
 
+// Tree keys 1 / 2: the centroid sort only has to bring each equal-centroid group together for k_group
+// (the tree order comes from the second sort, whose values are the input indices again), so its key is
+// a 31-bit hash of the centroid's bits (zeros canonical: -0 == +0 for the group test) and the sort runs
+// over 32 bits, four radix passes instead of eight; invalid beams carry 0xffffffff and sort last.  A
+// hash collision only lengthens k_group's equal-key run scan, which tests the centroids themselves.
+__device__ __forceinline__ unsigned int mix32(unsigned int h) {
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+__global__ __launch_bounds__(kBlock) void k_cent_hash(const float *__restrict__ box, const float *__restrict__ cent,
+                                                      int64_t n, unsigned long long *__restrict__ keys,
+                                                      int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float b[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = box[6 * i + k];
+    const float c[3] = {cent[3 * i], cent[3 * i + 1], cent[3 * i + 2]};
+    unsigned long long key = 0xffffffffull;
+    if (finite6(b) && isfinite(c[0]) && isfinite(c[1]) && isfinite(c[2])) {
+        unsigned int u[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) u[k] = c[k] == 0.0f ? 0u : __float_as_uint(c[k]);
+        key = mix32(u[0] ^ mix32(u[1] ^ mix32(u[2] + 0x9e3779b9u))) >> 1;
+    }
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
 // Tree order (BuildBuffers::beam_key 1 and 2): a 60-bit key of the beam's start AND
 // end point (10 bits each, in the box of all valid beams' end points), so a leaf tile holds beams
 // with both ends close -- a coherent bundle of nearly parallel, nearly coincident segments -- instead
@@ -491,6 +524,12 @@ hipError_t launch_morton(const BuildBuffers &b, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_cent_hash(const BuildBuffers &b, hipStream_t s) {
+    if (b.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cent_hash, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b.box, b.cent, b.n, b.keys, b.vals);
+    return hipGetLastError();
+}
+
 hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     if (nvalid > 0)
@@ -508,12 +547,12 @@ size_t sort_temp_bytes(int64_t n) {
     return bytes;
 }
 
-hipError_t launch_sort(const BuildBuffers &b, hipStream_t s) {
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit) {
     if (b.n == 0) return hipSuccess;
     size_t bytes = b.sort_tmp_bytes;
-    // Morton keys use bits [0, 63); invalid beams carry ~0 and sort last either way.
-    return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n, 0, 64,
-                                     s);
+    // Morton keys use bits [0, 63), the centroid hash bits [0, 32); invalid beams sort last either way.
+    return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n, 0,
+                                     (unsigned int)end_bit, s);
 }
 
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {

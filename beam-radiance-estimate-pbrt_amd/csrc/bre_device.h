@@ -124,7 +124,9 @@ static_assert(sizeof(ChunkRec) == 64, "ChunkRec must be one 64-B line");
 hipError_t launch_prep(const BuildBuffers &b, hipStream_t s);
 hipError_t launch_morton(const BuildBuffers &b, hipStream_t s);
 size_t sort_temp_bytes(int64_t n);
-hipError_t launch_sort(const BuildBuffers &b, hipStream_t s);
+// tree keys 1 / 2: a hash of the centroid for the equal-centroid groups (sorted over 32 bits)
+hipError_t launch_cent_hash(const BuildBuffers &b, hipStream_t s);
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit = 64);
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 // tree key 1, after the centroid sort: group boxes (k_group), then the (start, end) keys into keys/vals
 hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
