@@ -314,6 +314,8 @@ __global__ __launch_bounds__(kBlock) void k_group(const float *__restrict__ box,
     }
 }
 
+// GROUP: the group boxes come from k_group (tree keys 1 / 2), so no centroid or key is read here
+template <bool GROUP>
 __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start, const float *__restrict__ end,
                                                  const float *__restrict__ radius, const float *__restrict__ power,
                                                  const float *__restrict__ box, const float *__restrict__ cent,
@@ -324,30 +326,32 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (s >= nvalid) return;
     const int32_t i = vals[s];
-    const unsigned long long key = keys[s];
-    const float *bx = gbox ? gbox : box;  // gbox: the group boxes of k_group (tree key 1)
+    const float *bx = GROUP ? gbox : box;  // gbox: the group boxes of k_group (tree keys 1 / 2)
     float lo[3] = {bx[6 * i], bx[6 * i + 1], bx[6 * i + 2]};
     float hi[3] = {bx[6 * i + 3], bx[6 * i + 4], bx[6 * i + 5]};
-    const float c0 = cent[3 * i], c1 = cent[3 * i + 1], c2 = cent[3 * i + 2];
-    // Tree key 0: the equal-centroid group (the reference's multi-beam SAH leaf), the union of the
-    // members' boxes; members share the centroid key, so they are within this key run.
-    for (int64_t t = s - 1; !gbox && t >= 0 && keys[t] == key; --t) {
-        const int32_t j = vals[t];
-        if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
+    if (!GROUP) {
+        const unsigned long long key = keys[s];
+        const float c0 = cent[3 * i], c1 = cent[3 * i + 1], c2 = cent[3 * i + 2];
+        // Tree key 0: the equal-centroid group (the reference's multi-beam SAH leaf), the union of the
+        // members' boxes; members share the centroid key, so they are within this key run.
+        for (int64_t t = s - 1; t >= 0 && keys[t] == key; --t) {
+            const int32_t j = vals[t];
+            if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                lo[k] = smin(lo[k], box[6 * j + k]);
-                hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = smin(lo[k], box[6 * j + k]);
+                    hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+                }
             }
         }
-    }
-    for (int64_t t = s + 1; !gbox && t < nvalid && keys[t] == key; ++t) {
-        const int32_t j = vals[t];
-        if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
+        for (int64_t t = s + 1; t < nvalid && keys[t] == key; ++t) {
+            const int32_t j = vals[t];
+            if (cent[3 * j] == c0 && cent[3 * j + 1] == c1 && cent[3 * j + 2] == c2) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                lo[k] = smin(lo[k], box[6 * j + k]);
-                hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = smin(lo[k], box[6 * j + k]);
+                    hi[k] = smax(hi[k], box[6 * j + 3 + k]);
+                }
             }
         }
     }
@@ -557,9 +561,12 @@ hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit) {
 
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {
     if (nvalid == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power, b.box,
-                       b.cent, b.keys_alt, b.vals_alt, nvalid, b.beam_key >= 1 ? b.gbox : nullptr, b.recs, b.pow,
-                       b.uniform_radius);
+    if (b.beam_key >= 1)
+        hipLaunchKernelGGL(k_pack<true>, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power,
+                           b.box, b.cent, b.keys_alt, b.vals_alt, nvalid, b.gbox, b.recs, b.pow, b.uniform_radius);
+    else
+        hipLaunchKernelGGL(k_pack<false>, dim3(grid_for(nvalid)), dim3(kBlock), 0, s, b.start, b.end, b.radius, b.power,
+                           b.box, b.cent, b.keys_alt, b.vals_alt, nvalid, nullptr, b.recs, b.pow, b.uniform_radius);
     return hipGetLastError();
 }
 

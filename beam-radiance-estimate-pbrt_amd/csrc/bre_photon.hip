@@ -294,18 +294,42 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
 }
 
 // The single-trace form's copy: photon i's first min(count, cap) beams from its slots to its offsets.
+// Each wave copies the beams of its 64 photons as one run: lane j takes the wave's j-th beam (owner by
+// a search of the wave's prefix sums in LDS), so the writes of consecutive lanes are consecutive and a
+// photon's slots are read together (a thread per photon strided its reads by cap slots: 0.27 ms at C2).
 __global__ __launch_bounds__(256) void k_photon_slots(int64_t n, int cap, const int32_t *__restrict__ counts,
                                                       const int64_t *__restrict__ offsets, const float *__restrict__ ss,
                                                       const float *__restrict__ se, const float *__restrict__ sr,
                                                       const float *__restrict__ sp, float *__restrict__ bs,
                                                       float *__restrict__ be, float *__restrict__ br,
                                                       float *__restrict__ bp) {
+    __shared__ int pre[4][65];      // per wave: exclusive prefix sums of the photons' copied beams
+    __shared__ int64_t off[4][64];  // per wave: the photons' output offsets
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int m = min(counts[i], cap);
-    const int64_t w = offsets[i];
-    for (int k = 0; k < m; ++k) {
-        const int64_t a = i * (int64_t)cap + k, b = w + k;
+    const int64_t i0 = i - lane;
+    const int m = i < n ? min(counts[i], cap) : 0;
+    int incl = m;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    pre[w][lane + 1] = incl;
+    if (lane == 0) pre[w][0] = 0;
+    off[w][lane] = i < n ? offsets[i] : 0;
+    __builtin_amdgcn_wave_barrier();
+    const int total = __shfl(incl, 63);
+    for (int j = lane; j < total; j += 64) {
+        int lo = 0, hi = 64;  // the photon p with pre[p] <= j < pre[p + 1]
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[w][mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        const int k = j - pre[w][lo];
+        const int64_t a = (i0 + lo) * (int64_t)cap + k, b = off[w][lo] + k;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             bs[3 * b + c] = ss[3 * a + c];
