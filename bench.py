@@ -813,6 +813,10 @@ class SceneWorkload:
                 "render_iterations": self.n_iter, "entry": ("bre_gather_camera" if a.entry == "camera" else
                                                             "bre_gather_device, recorder-order segments"),
                 "parallelism": (f"segment packets x{world} ({a.scaling} scaling), photons traced and camera pass "
+                                "on every rank, one RCCL gather of the ranks' packet-class film planes per written "
+                                "image (the 1-GPU film bit for bit)"
+                                if a.shard_mode == "packets" and film_classes(a) > 1 else
+                                f"segment packets x{world} ({a.scaling} scaling), photons traced and camera pass "
                                 "on every rank, one RCCL reduce of the partial films per written image"
                                 if a.shard_mode == "packets" else
                                 f"BVH work roots x{world} ({a.scaling} scaling), photons traced and camera pass "

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 run 15 / 16 (via gpurun): build changes (15: hash-keyed 32-bit centroid sort; 16: wave-run photon slot copy, k_pack without centroid reads) --
+# Round 5 run 15 / 16 (via gpurun): build changes (15: hash-keyed 32-bit centroid sort; 16: wave-run photon slot copy, k_pack without centroid reads; 17: leaf boxes one wave per leaf) --
 # build / group-box tests, per-segment sums bit for bit against HEAD's full native tree (variant
 # base), C2 N = 1 and emulated rank of 8 timing, A/B/A/B.
 set -o pipefail
