@@ -62,7 +62,8 @@ struct bre_ctx {
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
-    int tscan = 6;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
+    int tscan = 4;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
+                             // (round 5: 4 over 6, C2 +0.5%, C3 +4.8%, profiles/r5/run20, run22)
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
     int tile_axis = 1;       // internal (option 112): per-lane tile line reject (GatherArgs::tileax), 1 = on (default since round 4), 0 = off
