@@ -64,12 +64,6 @@ constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 #ifndef BRE_SQRT_NOSCALE
 #define BRE_SQRT_NOSCALE 1
 #endif
-// BRE_DIR_SPREAD 1: the packet line reject bounds the lanes' spread along the common normal of the
-// bundle line and the beam (an octagon of directional extents, make_bundle) instead of by the bundle's
-// radius (A/B)
-#ifndef BRE_DIR_SPREAD
-#define BRE_DIR_SPREAD 1
-#endif
 // The exact stage reads the SegRec planes through a buffer descriptor (SGPR base + 32-bit lane offset:
 // one VALU of address arithmetic instead of 64-bit pointer math; with the power too, C2 +0.8%, C3 +2%,
 // profiles/r3b/run4).
