@@ -988,8 +988,13 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         T.ab = 0.f;
         bool keep = false;
         if (lane < nb) {
+            // raised wave priority while the tile's records are requested: its loads issue ahead of
+            // the other waves' scan VALU (round 5: C2 +0.3%, C3 +0.5%, profiles/r5/run27; the same
+            // around the exact stage's loads measured -0.1%)
+            __builtin_amdgcn_s_setprio(2);
             const BeamV r = load_beam(recs, first + lane, bset);
             T = make_scan_beam(r, R, margin);
+            __builtin_amdgcn_s_setprio(0);
             // packet-level rejects (see make_bundle, bundle_box_miss): a beam far from every segment
             // of the packet, or whose box no lane's ray can reach, is skipped by all lanes
             keep = !prefilter ||
