@@ -28,6 +28,7 @@ OPT_COUNTERS, OPT_TIMING, OPT_KERNEL, OPT_LEAF_SIZE, OPT_SQRT_MODE, OPT_SPLIT, O
 OPT_SHARD_RANK, OPT_SHARD_COUNT, OPT_TILE_LEAF = 8, 9, 10
 OPT_CHUNK_LEN, OPT_CHUNK_LEAF, OPT_SORT_SEGMENTS, OPT_SHARD_BLOCK, OPT_SHARD_MODE = 11, 12, 13, 14, 15
 OPT_FILM_CLASSES, FILM_CLASSES = 16, 8
+EMPTY_CHILD = -(2 ** 31)  # kEmptyChild (bre_device.h): no child
 
 # Every entry point include/bre.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -163,6 +164,17 @@ def _ptr(a):
     return a.data_ptr()  # torch tensor
 
 
+def _check_device_f32(t, what: str):
+    """A device buffer handed to libbre as a raw pointer must be a contiguous float32 CUDA tensor: the
+    library reads and writes it as float[] on the device, so anything else is refused before a launch."""
+    import torch
+
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+        desc = (f"{t.dtype} on {t.device}, contiguous={t.is_contiguous()}" if isinstance(t, torch.Tensor)
+                else type(t).__name__)
+        raise ValueError(f"{what}: needs a contiguous float32 CUDA tensor, got {desc}")
+
+
 def _f32(a, n3=None):
     a = np.ascontiguousarray(a, dtype=np.float32)
     return a
@@ -231,13 +243,18 @@ class BeamGather:
         if n < need:
             raise ValueError(f"{what}: film of {n} floats, the context's {self._classes} film class(es) over "
                              f"{npix} pixels need {need}")
+        _check_device_f32(buf, what)
         return buf
 
     def resolve_classes(self, classes, out):
         """out (npix, 3) = the sum of the 8 class planes of `classes` ((8 * npix, 3) or (8, npix, 3),
         torch CUDA float32), added in class order on the context's stream."""
+        _check_device_f32(classes, "resolve_classes: classes")
+        _check_device_f32(out, "resolve_classes: out")
         npix = out.numel() // 3
-        assert classes.numel() == FILM_CLASSES * 3 * npix
+        if classes.numel() != FILM_CLASSES * 3 * npix:
+            raise ValueError(f"resolve_classes: {classes.numel()} floats of class planes for {npix} pixels, "
+                             f"need {FILM_CLASSES * 3 * npix}")
         self._check(self.lib.bre_resolve_classes(self.h, npix, _ptr(classes), _ptr(out)))
 
     def set_stream(self, stream_handle: int | None):
@@ -374,6 +391,20 @@ class BeamGather:
         self._check(self.lib.bre_device_check(self.h, kind, n, _ptr(x), 0 if a is None else a.shape[0],
                                               None if a is None else _ptr(a), _ptr(y)))
         return y
+
+    def work_roots(self, children, nleaf, S: int):
+        """bre_device_check kind 5: the tile kernel's S work roots (k_roots) of a binary tree given as
+        children [(c0, c1)] (>= 0 node, < 0 leaf ~k, EMPTY_CHILD none) and nleaf per node, node 0 the
+        root.  Returns the roots, largest first."""
+        m = len(children)
+        rec = np.zeros((m, 16), np.int32)
+        for i, (c0, c1) in enumerate(children):
+            rec[i, 12], rec[i, 13], rec[i, 14], rec[i, 15] = c0, c1, -1, nleaf[i]
+        x = rec.view(np.float32).ravel()
+        y = np.zeros(S + 1, np.int32)
+        a = np.array([S], np.float32)
+        self._check(self.lib.bre_device_check(self.h, 5, x.shape[0], _ptr(x), 1, _ptr(a), _ptr(y)))
+        return [int(v) for v in y[:int(y[S])]]
 
     def close(self):
         if getattr(self, "h", None):

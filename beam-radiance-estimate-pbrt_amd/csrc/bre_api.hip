@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <initializer_list>
 #include <thread>
 #include <vector>
 
@@ -18,6 +19,10 @@
 #include "bre_trace.h"
 
 using namespace bre;
+
+#ifndef BRE_KERNEL_READBACK
+#define BRE_KERNEL_READBACK 0
+#endif
 
 namespace {
 
@@ -79,6 +84,8 @@ struct bre_ctx {
     int beam_key = 2;        // internal: tree order of the build (BuildBuffers::beam_key): 2 / 1 (start, end) Hilbert / Morton, 0 centroid
     int64_t partial_cap = (int64_t)4 << 30;  // tile kernel: bytes of per-subtree partials per launch (4 GiB)
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
+    unsigned int *rb_host = nullptr;     // pinned words of read_small (kernel readback)
+    int kernel_readback = BRE_KERNEL_READBACK;  // internal (option 118): read_small through k_readback
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
     int chunk_len = 400;   // chunk length in units of E / 100
     int chunk_leaf = 1;    // chunks per LBVH leaf
@@ -153,6 +160,59 @@ bre_status fail(bre_ctx *c, bre_status st, const char *fmt, ...) {
 
 bre_status set_device(bre_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
+    return BRE_OK;
+}
+
+// Small device-to-host reads of the pass chain (the photon total, the build's valid count, the camera
+// pass's segment total, the sticky error flags), synchronising the context's stream.  With option 118
+// a one-wave kernel stores the words into pinned host memory; otherwise hipMemcpyAsync, whose copy
+// kernel (the runtime's own, with multi-wave workgroups) waited up to 32 ms for CUs behind a
+// concurrent gather's one-wave blocks in the round-5 pipelined trace.
+struct ReadSpans {
+    const unsigned int *src[4];
+    int words[4];
+    int n;
+};
+__global__ __launch_bounds__(64) void k_readback(ReadSpans r, unsigned int *__restrict__ dst) {
+    int o = 0;
+    for (int i = 0; i < r.n; ++i) {
+        if ((int)threadIdx.x < r.words[i]) dst[o + threadIdx.x] = r.src[i][threadIdx.x];
+        o += r.words[i];
+    }
+}
+struct HostSpan {
+    void *host;
+    const void *dev;
+    size_t bytes;  // a multiple of 4, <= 64 words over all spans
+};
+bre_status read_small(bre_ctx *c, std::initializer_list<HostSpan> spans) {
+    if (!c->kernel_readback) {
+        for (const HostSpan &h : spans)
+            HIPCHK(c, hipMemcpyAsync(h.host, h.dev, h.bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return BRE_OK;
+    }
+    if (!c->rb_host) {
+        void *h = nullptr;
+        HIPCHK(c, hipHostMalloc(&h, 64 * sizeof(unsigned int), hipHostMallocDefault));
+        c->rb_host = static_cast<unsigned int *>(h);
+    }
+    ReadSpans r{};
+    int tot = 0;
+    for (const HostSpan &h : spans) {
+        if (r.n == 4 || h.bytes % 4 || tot + (int)(h.bytes / 4) > 64) return fail(c, BRE_ERR_STATE, "read_small: bad span");
+        r.src[r.n] = static_cast<const unsigned int *>(h.dev);
+        r.words[r.n] = (int)(h.bytes / 4);
+        tot += r.words[r.n++];
+    }
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, c->stream, r, c->rb_host);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int o = 0;
+    for (const HostSpan &h : spans) {
+        memcpy(h.host, c->rb_host + o, h.bytes);
+        o += (int)(h.bytes / 4);
+    }
     return BRE_OK;
 }
 
@@ -252,8 +312,10 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
         HIPCHK(c, launch_sort(b, c->stream));
     }
     unsigned int nv[3] = {0u, 0u, 0u};  // valid beams, min / max of their radius bits (k_prep)
-    HIPCHK(c, hipMemcpyAsync(nv, b.nvalid, sizeof(nv), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    {
+        const bre_status rs = read_small(c, {{nv, b.nvalid, sizeof(nv)}});
+        if (rs != BRE_OK) return rs;
+    }
     const int64_t nvalid = nv[0];
     c->nvalid = nvalid;
     // one radius for every valid beam: the records carry the power instead (BeamRec, BeamSet)
@@ -458,8 +520,10 @@ bre_status check_flags(bre_ctx *c) {
         c->flags_host = static_cast<unsigned int *>(h);
     }
     unsigned int *dflags = &c->counters_buf.as<DevCounters>()->flags;
-    HIPCHK(c, hipMemcpyAsync(c->flags_host, dflags, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    {
+        const bre_status rs = read_small(c, {{c->flags_host, dflags, sizeof(unsigned int)}});
+        if (rs != BRE_OK) return rs;
+    }
     const unsigned int f = *c->flags_host;
     if (f == 0) return BRE_OK;
     HIPCHK(c, hipMemsetAsync(dflags, 0, sizeof(unsigned int), c->stream));
@@ -688,6 +752,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->chk_x, &c->chk_aux, &c->chk_y};
     for (DevMem *m : all) m->release();
     if (c->flags_host) (void)hipHostFree(c->flags_host);
+    if (c->rb_host) (void)hipHostFree(c->rb_host);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
@@ -813,6 +878,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 117:  // internal: photon / camera passes on a high-priority stream, 1 (default) / 0 on the caller's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "pass priority must be 0 or 1");
         c->pass_priority = (int)value;
+        return BRE_OK;
+    case 118:  // internal: small device-to-host reads by a one-wave kernel into pinned memory (1) / hipMemcpyAsync (0)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "readback mode must be 0 or 1");
+        c->kernel_readback = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
@@ -1061,9 +1130,8 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
     HIPCHK(c, launch_count_scan(c->ph_tmp.ptr, c->ph_tmp.cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
                                 n_photons, c->stream));
     int64_t total = 0;
-    HIPCHK(c, hipMemcpyAsync(&total, c->ph_offsets.as<int64_t>() + n_photons, sizeof(total), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    st = read_small(c, {{&total, c->ph_offsets.as<int64_t>() + n_photons, sizeof(total)}});
+    if (st != BRE_OK) return st;
     const size_t B = (size_t)total;
     if (total > 0) {
         HIPCHK(c, c->in_start.ensure(B * 3 * sizeof(float)));
@@ -1180,12 +1248,10 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     int64_t last_off = 0;
     int32_t last_valid = 0;
     unsigned int flags = 0;
-    HIPCHK(c, hipMemcpyAsync(&last_off, c->cam_offs.as<int64_t>() + (S - 1), sizeof(int64_t), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(&last_valid, c->cs_valid.as<int32_t>() + (S - 1), sizeof(int32_t),
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&flags, c->cam_flags.ptr, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    st = read_small(c, {{&last_off, c->cam_offs.as<int64_t>() + (S - 1), sizeof(int64_t)},
+                        {&last_valid, c->cs_valid.as<int32_t>() + (S - 1), sizeof(int32_t)},
+                        {&flags, c->cam_flags.ptr, sizeof(flags)}});
+    if (st != BRE_OK) return st;
     const int64_t n = last_off + last_valid;
     const size_t N = (size_t)(n > 0 ? n : 1);
     HIPCHK(c, c->seg_o.ensure(N * 3 * sizeof(float)));
@@ -1299,6 +1365,10 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
     const bool sortable = c->kernel == 0 || c->kernel == 4;
     if (c->film_classes > 1 && d_accum && (!sortable || !c->film_compose))
         return fail(c, BRE_ERR_STATE, "BRE_OPT_FILM_CLASSES needs the deterministic compose of kernels 0 / 4");
+    // work-root shards gather every segment against a subset of the subtrees: each rank's sums are partial in
+    // every class plane, so per-rank planes cannot be gathered plane by plane (dist.ShardedFrame refuses it too)
+    if (c->film_classes > 1 && d_accum && c->shard_mode == 2 && c->shard_count > 1)
+        return fail(c, BRE_ERR_STATE, "BRE_OPT_FILM_CLASSES needs packet shards (BRE_OPT_SHARD_MODE 1), not work-root shards");
     if (c->film_classes > 1 && d_accum && (uint64_t)BRE_FILM_CLASSES * (uint64_t)(npix + 1) > 0xffffffffull)
         return fail(c, BRE_ERR_INVALID_ARG, "BRE_OPT_FILM_CLASSES: the film is too large for the class keys");
     if (!d_accum || !sortable || n <= 0 || !pix || c->nvalid == 0 || !c->film_compose)
@@ -1770,8 +1840,25 @@ int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int3
 bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
                             float *y) {
     if (!c) return BRE_ERR_INVALID_ARG;
-    if (kind < 0 || kind > 4) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 4]", kind);
+    if (kind < 0 || kind > 5) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 5]", kind);
     if (n < 0 || (n > 0 && (!x || !y))) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: bad arrays");
+    if (kind == 5) {
+        // the tile kernel's work roots (k_roots) of a caller tree: x = n / 16 Node records as words
+        if (n_aux < 1 || !aux) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind 5 needs aux[0] = S");
+        const int S = (int)aux[0];
+        if (n < 16 || n % 16 || S < 1 || S > kMaxSplit || (S & (S - 1)))
+            return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind 5 needs whole Node records and S a power of two <= %d",
+                        kMaxSplit);
+        bre_status st = set_device(c);
+        if (st != BRE_OK) return st;
+        HIPCHK(c, c->chk_x.ensure((size_t)n * 4));
+        HIPCHK(c, c->chk_y.ensure((size_t)(S + 1) * 4));
+        HIPCHK(c, hipMemcpyAsync(c->chk_x.ptr, x, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, launch_roots(c->chk_x.as<Node>(), S, c->chk_y.as<int32_t>(), c->stream));
+        HIPCHK(c, hipMemcpyAsync(y, c->chk_y.ptr, (size_t)(S + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return BRE_OK;
+    }
     const bool need_aux = kind >= 3;
     if (need_aux && (n_aux < 1 || !aux)) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d needs aux", kind);
     if (n == 0) return BRE_OK;

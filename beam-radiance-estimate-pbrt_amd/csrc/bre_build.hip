@@ -52,7 +52,10 @@ __device__ __forceinline__ bool finite6(const float *b) {
     return ok;
 }
 
-constexpr int kBlock = 256;
+#ifndef BRE_PASS_BLOCK
+#define BRE_PASS_BLOCK 256
+#endif
+constexpr int kBlock = BRE_PASS_BLOCK;  // threads per block of the pass kernels
 
 __global__ void k_prep_init(unsigned int *__restrict__ cbounds, unsigned int *__restrict__ nvalid) {
     const int t = threadIdx.x;

@@ -1358,6 +1358,8 @@ struct RootsShared {
     int32_t fc[kMaxSplit + 1], fw[kMaxSplit + 1];  // the roots, unordered
     int cnt, lo, hi, nf;
 };
+// one block holds the whole cache: it must fit gfx950's 160 KB of LDS per CU (k_roots runs as one block)
+static_assert(sizeof(RootsShared) <= 160 * 1024, "k_roots: RootsShared exceeds the 160 KB of LDS of a gfx950 CU");
 
 // children, parent and leaf tiles of node x: the record's last 16 bytes
 __device__ __forceinline__ int4 node_tail(const Node *__restrict__ nodes, int32_t x) {

@@ -118,7 +118,10 @@ void prepare_scene(const bre_scene *s, HostScene *out, const float *d_density) {
 
 namespace {
 
-constexpr int kPhotonBlock = 128;
+#ifndef BRE_PHOTON_BLOCK
+#define BRE_PHOTON_BLOCK 128
+#endif
+constexpr int kPhotonBlock = BRE_PHOTON_BLOCK;
 
 // A path suspended at a medium scattering event while its scattered child is traced.
 struct Frame {

@@ -23,7 +23,10 @@ namespace bre {
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef BRE_PASS_BLOCK
+#define BRE_PASS_BLOCK 256
+#endif
+constexpr int kBlock = BRE_PASS_BLOCK;  // threads per block of the pass kernels
 
 __device__ __forceinline__ unsigned int f2ord(float f) {
     unsigned int u = __float_as_uint(f);
@@ -347,9 +350,10 @@ __global__ __launch_bounds__(kBlock) void k_seg_classes(int64_t n, int block, in
     cls[s] = (uint8_t)(((i >> 6) / block) % classes);
 }
 
-// The image of the class films, added in class order (bit-identical wherever the planes are).
-__global__ __launch_bounds__(kBlock) void k_resolve_classes(int64_t m, int classes, const float *__restrict__ in,
-                                                            float *__restrict__ out) {
+// The image of the class films, added in class order (bit-identical wherever the planes are).  `out` may
+// alias plane 0 of `in` (include/bre.h), so neither pointer is __restrict__: each thread reads its element
+// of every plane before it stores out[i].
+__global__ __launch_bounds__(kBlock) void k_resolve_classes(int64_t m, int classes, const float *in, float *out) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= m) return;
     float v = in[i];

@@ -57,23 +57,26 @@ class ShardedFrame:
     """Full-resolution RGB accumulation buffer of one rank (only its own tiles are ever written)."""
 
     def __init__(self, w: int, h: int, rank: int, world: int, device="cpu", tile: int = 16, block: int = 1,
-                 packets: bool = False, classes: int = 1):
+                 packets: bool = False, classes: int = 1, roots: bool = False):
         import torch
 
         self.w, self.h, self.rank, self.world, self.tile, self.block = w, h, rank, world, tile, block
         # packets=True: PACKET shards (BRE_OPT_SHARD_MODE 1) -- every rank may write every pixel (its
         # range of the sorted segment packets), and the films are SUMMED by one reduce, or, with
-        # classes=8 (packet-class films), gathered plane by plane
-        self.packets = packets
-        if classes != 1 and not packets:
-            raise ValueError("packet-class films need packet shards")
+        # classes=8 (packet-class films), gathered plane by plane.  roots=True: WORK-ROOT shards
+        # (BRE_OPT_SHARD_MODE 2) -- every rank writes partial sums of every pixel in every plane, so only
+        # the sum-reduce combines them (libbre refuses class films under root shards as well)
+        self.roots = roots
+        self.packets = packets or roots
+        if classes != 1 and (roots or not packets):
+            raise ValueError("packet-class films need packet shards (not tile or work-root shards)")
         self.classes = classes
-        self.pixels = np.arange(w * h, dtype=np.int64) if packets else tile_pixels(w, h, rank, world, tile, block)
+        self.pixels = np.arange(w * h, dtype=np.int64) if self.packets else tile_pixels(w, h, rank, world, tile, block)
         # with classes: (classes * w * h, 3), plane c = rows [c * w * h, (c + 1) * w * h)
         self.accum = torch.zeros((classes * w * h, 3), dtype=torch.float32, device=device)
         self.device = device
         self._band = None
-        if not packets:  # the band machinery (also at world 1: a live 1-rank group still runs the gather)
+        if not self.packets:  # the band machinery (also at world 1: a live 1-rank group still runs the gather)
             counts = [tile_pixels(w, h, r, world, tile, block).shape[0] for r in range(world)]
             self.band_len = max(counts)
             self._idx = torch.from_numpy(self.pixels).to(device)
@@ -121,7 +124,7 @@ class ShardedFrame:
         live = dist.is_available() and dist.is_initialized()
         if self.world == 1 and not live:
             return self.accum
-        if self.packets and self.classes > 1 and self.classes % self.world == 0:
+        if self.packets and not self.roots and self.classes > 1 and self.classes % self.world == 0:
             return self._gather_planes(root)
         if self.packets:  # partial films of one image: one sum-reduce to the root
             if dist.get_backend() == "gloo" and self.accum.is_cuda:  # gloo reduces host tensors

@@ -214,7 +214,8 @@ def main():
         srank, scount = (int(x) for x in args.emulate_shard.split("/"))
     classes = film_classes(args)
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
-                              packets=args.shard_mode in ("packets", "roots"), classes=classes)
+                              packets=args.shard_mode == "packets", roots=args.shard_mode == "roots",
+                              classes=classes)
     def make_ctx():
         return make_context(bre, args, dev)
 

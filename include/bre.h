@@ -159,7 +159,13 @@ const char *bre_last_error(const bre_ctx *ctx);
 int bre_abi_version(void);
 bre_status bre_set_option(bre_ctx *ctx, int option, int64_t value);
 /* Use an existing hipStream_t (cast to void*) for all work of this context; NULL = the
-   context's own stream.  The caller keeps ownership of a stream it passes in. */
+   context's own stream.  The caller keeps ownership of a stream it passes in.
+   The photon pass (with its BVH build) and the camera pass run on an internal stream of the device's
+   highest priority (internal option 117, on by default), forked from this stream -- the pass starts
+   after everything queued on it before the call -- and joined back to it before the call returns, so
+   work queued on this stream afterwards waits for the pass: stream order towards the caller is exactly
+   as if the pass ran on this stream (tests/test_pass_stream_gpu.py reuses a freed film right after
+   each pass, with the option on and off). */
 bre_status bre_set_stream(bre_ctx *ctx, void *hip_stream);
 bre_status bre_synchronize(bre_ctx *ctx);
 bre_status bre_get_stats(const bre_ctx *ctx, bre_stats *out);
@@ -315,6 +321,9 @@ bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, f
              light choice of Distribution1D::SampleDiscrete, sampling.h:90-100)
      kind 4: y[2i] = x / aux[0] by the exact stage's shared-reciprocal division (div_by_shared),
              y[2i+1] = x / aux[0] correctly rounded
+     kind 5: the tile kernel's S = aux[0] work roots (k_roots) of the binary tree whose n / 16 Node
+             records (bre_device.h: only child[2] and nleaf are read) are x's words; y receives S + 1
+             int32 words: the roots largest first (kEmptyChild-padded), then their count
    so the tests can hold them against the reference's own primitive tests (src/tests/fp_tests.cpp,
    find_interval.cpp) and against the compiler's correctly rounded sqrt and division. */
 bre_status bre_device_check(bre_ctx *ctx, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,

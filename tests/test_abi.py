@@ -71,10 +71,17 @@ def test_film_buffers_are_checked_against_the_film_classes(bre):
     class Ctx:
         _classes = bre.FILM_CLASSES
 
-    film = np.zeros((8 * 100, 3), np.float32)
-    assert bre.BeamGather._film(Ctx(), film, 100, "t") is film
-    with pytest.raises(ValueError):
+    import torch
+
+    with pytest.raises(ValueError, match="film of"):
         bre.BeamGather._film(Ctx(), np.zeros((100, 3), np.float32), 100, "t")
+    # the right size, but not a contiguous float32 CUDA tensor: refused before any raw-pointer use
+    # (the CUDA case itself is exercised by every GPU test that passes a film)
+    for bad in (np.zeros((8 * 100, 3), np.float32), torch.zeros((8 * 100, 3), dtype=torch.float32),
+                torch.zeros((8 * 100, 3), dtype=torch.float64), torch.zeros((3, 8 * 100)).t()):
+        with pytest.raises(ValueError, match="CUDA tensor"):
+            bre.BeamGather._film(Ctx(), bad, 100, "t")
     Ctx._classes = 1
-    assert bre.BeamGather._film(Ctx(), np.zeros((100, 3), np.float32), 100, "t") is not None
+    with pytest.raises(ValueError, match="CUDA tensor"):
+        bre.BeamGather._film(Ctx(), np.zeros((100, 3), np.float32), 100, "t")
     assert bre.BeamGather._film(Ctx(), None, 100, "t") is None

@@ -106,3 +106,25 @@ def test_empty_packet_shard_on_a_fresh_context(bre, scene_mod_gpu):
         g.gather_camera(0.02, film)
         g.synchronize()
         assert float(film.abs().sum()) == 0.0  # no segment of this shard (the surfaces went nowhere: no buffer)
+
+
+def test_root_shards_refuse_film_classes(bre, scene_mod_gpu):
+    """Packet-class films gather each rank's planes whole (dist.ShardedFrame._gather_planes): under
+    work-root shards every rank writes partial sums into every plane, so the gather would drop most
+    contributions.  The library refuses the combination with BRE_ERR_STATE, and so does
+    ShardedFrame (tests/test_dist.py)."""
+    import torch
+
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+    with bre.BeamGather(0) as g:
+        g.set_shard(0, 2, roots=True)
+        g.set_film_classes(bre.FILM_CLASSES)
+        g.trace_photons(scene, 5000, 0, 5, 0.02)
+        n = g.camera_pass(scene, 32, 32, 0, 5, True, True,
+                          surface=torch.zeros((bre.FILM_CLASSES * 32 * 32, 3), dtype=torch.float32, device="cuda"))
+        assert n > 0
+        film = torch.zeros((bre.FILM_CLASSES * 32 * 32, 3), dtype=torch.float32, device="cuda")
+        with pytest.raises(bre.BreError) as e:
+            g.gather_camera(0.02, film)
+            g.synchronize()
+        assert e.value.status == 4  # BRE_ERR_STATE
