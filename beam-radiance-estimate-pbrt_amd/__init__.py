@@ -39,7 +39,7 @@ EXPORTS = [
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
     "bre_render_progressive", "bre_shard_segments", "bre_set_beams_sharded", "bre_gather_sharded",
-    "bre_device_check", "bre_resolve_classes",
+    "bre_device_check", "bre_resolve_classes", "bre_film_add", "bre_set_gather_after",
 ]
 
 
@@ -148,6 +148,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if hasattr(lib, "bre_resolve_classes"):  # (absent from round-4 libraries loaded for A/B timing)
         lib.bre_resolve_classes.argtypes = [P, I64, P, P]
         lib.bre_resolve_classes.restype = I32
+    if hasattr(lib, "bre_film_add"):  # (absent from round-5 libraries loaded for A/B timing)
+        lib.bre_film_add.argtypes = [P, I64, P, P, I32]
+        lib.bre_film_add.restype = I32
+        lib.bre_set_gather_after.argtypes = [P, P]
+        lib.bre_set_gather_after.restype = I32
     if hasattr(lib, "bre_device_check"):  # (absent from round-3 libraries loaded for A/B timing)
         lib.bre_device_check.argtypes = [P, I32, I64, P, I32, P, P]
         lib.bre_device_check.restype = I32
@@ -256,6 +261,21 @@ class BeamGather:
             raise ValueError(f"resolve_classes: {classes.numel()} floats of class planes for {npix} pixels, "
                              f"need {FILM_CLASSES * 3 * npix}")
         self._check(self.lib.bre_resolve_classes(self.h, npix, _ptr(classes), _ptr(out)))
+
+    def film_add(self, src, dst, clear_src: bool = False):
+        """dst += src (torch CUDA float32 tensors of one size), then src = 0 if clear_src, on the
+        context's stream (bre_film_add: a one-wave kernel that runs beside another context's gather)."""
+        _check_device_f32(src, "film_add src")
+        _check_device_f32(dst, "film_add dst")
+        if src.numel() != dst.numel():
+            raise ValueError(f"film_add: {src.numel()} vs {dst.numel()} floats")
+        self._check(self.lib.bre_film_add(self.h, src.numel(), _ptr(src), _ptr(dst), int(bool(clear_src))))
+
+    def set_gather_after(self, prev: "BeamGather | None"):
+        """bre_set_gather_after: this context's tile kernels start after prev's last one (pipelined
+        contexts on one device; None clears)."""
+        self._after = prev  # prev must outlive the gathers that wait for it
+        self._check(self.lib.bre_set_gather_after(self.h, prev.h if prev is not None else None))
 
     def set_stream(self, stream_handle: int | None):
         self._check(self.lib.bre_set_stream(self.h, stream_handle))
@@ -390,6 +410,31 @@ class BeamGather:
         a = None if aux is None else np.ascontiguousarray(aux, dtype=np.float32)
         self._check(self.lib.bre_device_check(self.h, kind, n, _ptr(x), 0 if a is None else a.shape[0],
                                               None if a is None else _ptr(a), _ptr(y)))
+        return y
+
+    def slot_sort(self, keys, begin_bit: int = 0, end_bit: int | None = None):
+        """bre_device_check kinds 6 / 8: the pass chain's stable radix sort (bre_slot.hip) of uint64 or
+        uint32 keys; returns (sorted keys, the permutation)."""
+        k = np.ascontiguousarray(keys)
+        kb = k.dtype.itemsize
+        if k.dtype not in (np.uint64, np.uint32):
+            raise ValueError("slot_sort: uint64 or uint32 keys")
+        m = k.shape[0]
+        end_bit = 8 * kb if end_bit is None else end_bit
+        x = k.view(np.uint32)
+        y = np.zeros(m * (kb + 4) // 4 + 1, np.uint32)
+        a = np.array([begin_bit, end_bit], np.float32)
+        self._check(self.lib.bre_device_check(self.h, 6 if kb == 8 else 8, x.shape[0], _ptr(x), 2, _ptr(a), _ptr(y)))
+        sk = y[: m * kb // 4].view(k.dtype).copy()
+        perm = y[m * kb // 4: m * kb // 4 + m].view(np.int32).copy()
+        return sk, perm
+
+    def slot_scan(self, values):
+        """bre_device_check kind 7: the pass chain's exclusive scan (bre_slot.hip) of int32 values;
+        returns int64 [n + 1] (the total last)."""
+        v = np.ascontiguousarray(values, dtype=np.int32)
+        y = np.zeros(v.shape[0] + 1, np.int64)
+        self._check(self.lib.bre_device_check(self.h, 7, v.shape[0], _ptr(v), 0, None, _ptr(y)))
         return y
 
     def work_roots(self, children, nleaf, S: int):

@@ -21,7 +21,7 @@
 using namespace bre;
 
 #ifndef BRE_KERNEL_READBACK
-#define BRE_KERNEL_READBACK 0
+#define BRE_KERNEL_READBACK 1
 #endif
 
 namespace {
@@ -86,6 +86,8 @@ struct bre_ctx {
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     unsigned int *rb_host = nullptr;     // pinned words of read_small (kernel readback)
     int kernel_readback = BRE_KERNEL_READBACK;  // internal (option 118): read_small through k_readback
+    int slot_passes = 1;  // internal (option 119): the pass chain's scans, sorts and fills by the one-wave
+                          // primitives (bre_slot.hip, default) / 0 rocPRIM and hipMemsetAsync (A/B)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
     int chunk_len = 400;   // chunk length in units of E / 100
     int chunk_leaf = 1;    // chunks per LBVH leaf
@@ -107,7 +109,7 @@ struct bre_ctx {
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem chk_x, chk_aux, chk_y;  // bre_device_check staging
-    DevMem counters_buf, roots, roots_sh, partial, pcnt, segrec, tileax, segbox, nodes4;
+    DevMem counters_buf, roots, roots_sh, roots_tmp, partial, pcnt, segrec, tileax, segbox, nodes4;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     DevMem ph_s_start, ph_s_end, ph_s_radius, ph_s_power;  // single-trace photon pass: per-photon beam slots
@@ -136,6 +138,10 @@ struct bre_ctx {
     int pass_priority = 1;
     hipStream_t pstream = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    // bre_set_gather_after: this context's tile kernels wait for `after`'s last one (after->tile_ev)
+    bre_ctx *after = nullptr;
+    hipEvent_t tile_ev = nullptr;  // recorded after each tile-kernel launch (created on first use)
+    bool tile_ev_valid = false;
 };
 
 namespace {
@@ -161,6 +167,14 @@ bre_status fail(bre_ctx *c, bre_status st, const char *fmt, ...) {
 bre_status set_device(bre_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
     return BRE_OK;
+}
+
+// Zero `bytes` (a multiple of 4) of device memory on the context's stream: a one-wave fill kernel
+// (bre_slot.hip) instead of hipMemsetAsync's runtime kernel, which waits for CUs behind a concurrent
+// gather (the pipelined pass chain); option 119 = 0 keeps hipMemsetAsync.
+hipError_t fill_words(bre_ctx *c, void *p, size_t bytes) {
+    if (!c->slot_passes || bytes % 4) return hipMemsetAsync(p, 0, bytes, c->stream);
+    return slot_fill(p, (int64_t)(bytes / 4), 0u, c->stream);
 }
 
 // Small device-to-host reads of the pass chain (the photon total, the build's valid count, the camera
@@ -287,6 +301,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
     b.power = power;
     b.n = n;
     b.sqrt_mode = c->sqrt_mode;
+    b.slot = c->slot_passes;
     b.leaf_size = c->leaf_size;
     b.beam_key = c->beam_key;
     b.box = c->box.as<float>();
@@ -369,7 +384,8 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
         // the tile kernel's work roots and 4-wide view, here on the build's stream: with two contexts
         // pipelined they overlap the other context's gather instead of preceding this one's
         HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
-        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
+        HIPCHK(c, c->roots_tmp.ensure(roots_scratch_bytes()));
+        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->roots_tmp.ptr, c->stream));
         c->roots_split = c->split;
         HIPCHK(c, c->nodes4.ensure(sizeof(Node4) * (size_t)nnodes));
         HIPCHK(c, launch_collapse4(c->nodes.as<Node>(), nnodes, c->nodes4.as<Node4>(), c->stream));
@@ -499,10 +515,11 @@ bre_status gather_chunk(bre_ctx *c, const GatherArgs &a) {
 bre_status counters_block(bre_ctx *c, DevCounters **out) {
     if (!c->counters_buf.ptr) {
         HIPCHK(c, c->counters_buf.ensure(sizeof(DevCounters)));
-        HIPCHK(c, hipMemsetAsync(c->counters_buf.ptr, 0, sizeof(DevCounters), c->stream));
+        HIPCHK(c, fill_words(c, c->counters_buf.ptr, sizeof(DevCounters)));
     }
     *out = c->counters_buf.as<DevCounters>();
-    HIPCHK(c, hipMemsetAsync(*out, 0, offsetof(DevCounters, flags), c->stream));
+    static_assert(offsetof(DevCounters, flags) % 4 == 0, "DevCounters: word-aligned flags");
+    HIPCHK(c, fill_words(c, *out, offsetof(DevCounters, flags)));
     return BRE_OK;
 }
 
@@ -526,7 +543,7 @@ bre_status check_flags(bre_ctx *c) {
     }
     const unsigned int f = *c->flags_host;
     if (f == 0) return BRE_OK;
-    HIPCHK(c, hipMemsetAsync(dflags, 0, sizeof(unsigned int), c->stream));
+    HIPCHK(c, fill_words(c, dflags, sizeof(unsigned int)));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (f & kFlagStack)
         return fail(c, BRE_ERR_STATE, "bre_gather: traversal stack overflow (BVH deeper than the stack): contributions "
@@ -615,7 +632,8 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     HIPCHK(c, c->roots.ensure(sizeof(int32_t) * (kMaxSplit + 1)));
     HIPCHK(c, c->partial.ensure(sizeof(float) * 3 * (size_t)chunk * (size_t)S_eff));
     if (c->roots_split != c->split) {
-        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->stream));
+        HIPCHK(c, c->roots_tmp.ensure(roots_scratch_bytes()));
+        HIPCHK(c, launch_roots(c->nodes.as<Node>(), c->split, c->roots.as<int32_t>(), c->roots_tmp.ptr, c->stream));
         c->roots_split = c->split;
     }
     if (!c->nodes4_ok) {
@@ -648,8 +666,13 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         a.segbox = c->segbox.as<unsigned int>();
     }
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    if (!c->tile_ev) HIPCHK(c, hipEventCreateWithFlags(&c->tile_ev, hipEventDisableTiming));
     for (int64_t off = 0; off < nseg; off += chunk) {
         GatherArgs ac = a;
+        // pipelined contexts (bre_set_gather_after): the first launch waits for the other context's last
+        // tile kernel, the last one marks this context's
+        ac.wait_ev = (off == 0 && c->after && c->after->tile_ev_valid) ? c->after->tile_ev : nullptr;
+        ac.done_ev = off + chunk >= nseg ? c->tile_ev : nullptr;
         ac.nseg = std::min(chunk, nseg - off);
         ac.o = o + 3 * off;
         ac.p = p + 3 * off;
@@ -664,6 +687,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         }
         HIPCHK(c, launch_gather(ac, kernel, c->counters, c->stream));
     }
+    c->tile_ev_valid = true;
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
     return read_counters(c, a.ctr);
 }
@@ -697,7 +721,7 @@ bre_status read_counters(bre_ctx *c, DevCounters *ctr) {
 // exclusive scan of the camera slots' valid flags into cam_offs
 hipError_t rocprim_free_total_scan(bre_ctx *c, const CamSlots &cs, int64_t nslots, int max_depth) {
     return launch_camera_scan(c->cam_tmp.ptr, c->cam_tmp.cap, cs, nslots, max_depth, c->cam_offs.as<int64_t>(),
-                              c->stream);
+                              c->stream, c->slot_passes != 0);
 }
 
 }  // namespace
@@ -738,7 +762,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
                      &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
-                     &c->tileax, &c->segbox, &c->nodes4, &c->roots_sh,
+                     &c->tileax, &c->segbox, &c->nodes4, &c->roots_sh, &c->roots_tmp,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->ph_s_start, &c->ph_s_end, &c->ph_s_radius, &c->ph_s_power, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
                      &c->cam_tmp, &c->cam_flags, &c->seg_o, &c->seg_p, &c->seg_d, &c->seg_t, &c->seg_pix,
@@ -756,6 +780,7 @@ void bre_destroy(bre_ctx *c) {
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->tile_ev) (void)hipEventDestroy(c->tile_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     if (c->pstream) {
         (void)hipStreamSynchronize(c->pstream);
@@ -882,6 +907,10 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 118:  // internal: small device-to-host reads by a one-wave kernel into pinned memory (1) / hipMemcpyAsync (0)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "readback mode must be 0 or 1");
         c->kernel_readback = (int)value;
+        return BRE_OK;
+    case 119:  // internal: pass-chain scans / sorts / fills, 1 one-wave primitives (default) / 0 rocPRIM (A/B)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "pass primitives mode must be 0 or 1");
+        c->slot_passes = (int)value;
         return BRE_OK;
     case 111:  // internal: tile kernel prefilter margins, 1 tight (default) / 0 round 2's (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "margin mode must be 0 or 1");
@@ -1128,7 +1157,7 @@ bre_status bre_trace_photons(bre_ctx *c, const bre_scene *scene, int64_t n_photo
                                  nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, c->stream));
     }
     HIPCHK(c, launch_count_scan(c->ph_tmp.ptr, c->ph_tmp.cap, c->ph_counts.as<int32_t>(), c->ph_offsets.as<int64_t>(),
-                                n_photons, c->stream));
+                                n_photons, c->stream, c->slot_passes != 0));
     int64_t total = 0;
     st = read_small(c, {{&total, c->ph_offsets.as<int64_t>() + n_photons, sizeof(total)}});
     if (st != BRE_OK) return st;
@@ -1234,7 +1263,7 @@ bre_status bre_camera_pass(bre_ctx *c, const bre_scene *scene, int32_t width, in
     const size_t tmp = camera_scan_temp_bytes((int64_t)S);
     HIPCHK(c, c->cam_tmp.ensure(tmp + 16));
     HIPCHK(c, c->cam_flags.ensure(sizeof(unsigned int)));
-    HIPCHK(c, hipMemsetAsync(c->cam_flags.ptr, 0, sizeof(unsigned int), c->stream));
+    HIPCHK(c, fill_words(c, c->cam_flags.ptr, sizeof(unsigned int)));
     CamSlots cs{c->cs_o.as<float>(), c->cs_p.as<float>(), c->cs_d.as<float>(), c->cs_t.as<float>(),
                 c->cs_pix.as<int32_t>(), c->cs_valid.as<int32_t>()};
     if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
@@ -1344,7 +1373,7 @@ static bre_status gather_segments_core(bre_ctx *c, int64_t n, const float *o, co
     SegSort ss{n, o, p, d, t, pix, c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
                c->ss_keys_alt.as<unsigned long long>(), c->ss_vals.as<int32_t>(), c->ss_vals_alt.as<int32_t>(),
                c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
-               c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key};
+               c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key, c->slot_passes};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
     // ss_vals_alt[i] = the caller's index of sorted segment i (the sort's permutation)
     if (pshard) return pick(ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, c->ss_vals_alt.as<int32_t>());
@@ -1406,7 +1435,7 @@ static bre_status gather_segments(bre_ctx *c, int64_t n, const float *o, const f
     }
     PixelCompose pc{n, pix, segbuf, npix, d_accum, cls, c->film_classes, c->px_keys.as<unsigned int>(),
                     c->px_keys_alt.as<unsigned int>(), c->px_vals.as<int32_t>(), c->px_vals_alt.as<int32_t>(),
-                    c->px_tmp.ptr, tb, &ctr->flags, kFlagPixel};
+                    c->px_tmp.ptr, tb, &ctr->flags, kFlagPixel, c->slot_passes};
     HIPCHK(c, launch_pixel_compose(pc, c->stream));
     return BRE_OK;
 }
@@ -1427,6 +1456,24 @@ bre_status bre_resolve_classes(bre_ctx *c, int64_t npix, const float *d_classes,
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     HIPCHK(c, launch_resolve_classes(3 * npix, BRE_FILM_CLASSES, d_classes, d_out, c->stream));
+    return BRE_OK;
+}
+
+bre_status bre_set_gather_after(bre_ctx *c, bre_ctx *prev) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (prev == c || (prev && prev->device != c->device))
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_set_gather_after: another context of the same device");
+    c->after = prev;
+    return BRE_OK;
+}
+
+bre_status bre_film_add(bre_ctx *c, int64_t n_floats, float *d_src, float *d_dst, int32_t clear_src) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    if (n_floats < 0 || (n_floats > 0 && (!d_src || !d_dst)) || d_src == d_dst)
+        return fail(c, BRE_ERR_INVALID_ARG, "bre_film_add: bad films");
+    bre_status st = set_device(c);
+    if (st != BRE_OK) return st;
+    HIPCHK(c, launch_film_add(n_floats, d_src, d_dst, clear_src != 0, c->stream));
     return BRE_OK;
 }
 
@@ -1840,8 +1887,52 @@ int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int3
 bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
                             float *y) {
     if (!c) return BRE_ERR_INVALID_ARG;
-    if (kind < 0 || kind > 5) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 5]", kind);
+    if (kind < 0 || kind > 8) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 8]", kind);
     if (n < 0 || (n > 0 && (!x || !y))) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: bad arrays");
+    if (kind >= 6) {
+        // the pass chain's one-wave primitives (bre_slot.hip) on caller data
+        bre_status st = set_device(c);
+        if (st != BRE_OK) return st;
+        if (n == 0) return BRE_OK;
+        if (kind == 7) {  // exclusive scan of n int32 words; y: n + 1 int64 (the total last)
+            HIPCHK(c, c->chk_x.ensure((size_t)n * 4));
+            HIPCHK(c, c->chk_y.ensure((size_t)(n + 1) * 8));
+            HIPCHK(c, c->chk_aux.ensure(slot_scan_temp_bytes(n)));
+            HIPCHK(c, hipMemcpyAsync(c->chk_x.ptr, x, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, slot_exclusive_scan(c->chk_x.as<int32_t>(), c->chk_y.as<int64_t>(), n, c->chk_y.as<int64_t>() + n,
+                                          c->chk_aux.ptr, c->stream));
+            HIPCHK(c, hipMemcpyAsync(y, c->chk_y.ptr, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            return BRE_OK;
+        }
+        // kind 6 / 8: stable sort of m = n / 2 64-bit (n 32-bit) keys by bits [aux[0], aux[1]), values = the
+        // input positions; y: the sorted keys, then the values
+        if (n_aux < 2 || !aux) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kinds 6 / 8 need aux[0..1] bits");
+        const int kb = kind == 6 ? 8 : 4;
+        if ((n * 4) % kb) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind 6 needs an even word count");
+        const int64_t m = n * 4 / kb;
+        const size_t tb = slot_sort_temp_bytes(m, kb);
+        HIPCHK(c, c->chk_x.ensure((size_t)m * (kb + 4) * 2 + tb + 512));
+        char *base = static_cast<char *>(c->chk_x.ptr);
+        char *k0 = base, *k1 = k0 + (size_t)m * kb, *v0 = k1 + (size_t)m * kb, *v1 = v0 + (size_t)m * 4;
+        void *tmp = v1 + ((size_t)m * 4 + 256) / 256 * 256;
+        std::vector<int32_t> idx((size_t)m);
+        for (int64_t i = 0; i < m; ++i) idx[(size_t)i] = (int32_t)i;
+        HIPCHK(c, hipMemcpyAsync(k0, x, (size_t)m * kb, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(v0, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice, c->stream));
+        const int b0 = (int)aux[0], b1 = (int)aux[1];
+        if (kb == 8)
+            HIPCHK(c, slot_sort_pairs(tmp, reinterpret_cast<unsigned long long *>(k0), reinterpret_cast<unsigned long long *>(k1),
+                                      reinterpret_cast<int32_t *>(v0), reinterpret_cast<int32_t *>(v1), m, b0, b1, c->stream));
+        else
+            HIPCHK(c, slot_sort_pairs(tmp, reinterpret_cast<unsigned int *>(k0), reinterpret_cast<unsigned int *>(k1),
+                                      reinterpret_cast<int32_t *>(v0), reinterpret_cast<int32_t *>(v1), m, b0, b1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(y, k1, (size_t)m * kb, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(reinterpret_cast<char *>(y) + (size_t)m * kb, v1, (size_t)m * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return BRE_OK;
+    }
     if (kind == 5) {
         // the tile kernel's work roots (k_roots) of a caller tree: x = n / 16 Node records as words
         if (n_aux < 1 || !aux) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind 5 needs aux[0] = S");
@@ -1854,7 +1945,8 @@ bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x,
         HIPCHK(c, c->chk_x.ensure((size_t)n * 4));
         HIPCHK(c, c->chk_y.ensure((size_t)(S + 1) * 4));
         HIPCHK(c, hipMemcpyAsync(c->chk_x.ptr, x, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, launch_roots(c->chk_x.as<Node>(), S, c->chk_y.as<int32_t>(), c->stream));
+        HIPCHK(c, c->roots_tmp.ensure(roots_scratch_bytes()));
+        HIPCHK(c, launch_roots(c->chk_x.as<Node>(), S, c->chk_y.as<int32_t>(), c->roots_tmp.ptr, c->stream));
         HIPCHK(c, hipMemcpyAsync(y, c->chk_y.ptr, (size_t)(S + 1) * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         return BRE_OK;

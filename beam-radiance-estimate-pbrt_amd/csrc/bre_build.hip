@@ -53,7 +53,7 @@ __device__ __forceinline__ bool finite6(const float *b) {
 }
 
 #ifndef BRE_PASS_BLOCK
-#define BRE_PASS_BLOCK 256
+#define BRE_PASS_BLOCK 64  // one wave (bre_slot.hip; 256 until round 5)
 #endif
 constexpr int kBlock = BRE_PASS_BLOCK;  // threads per block of the pass kernels
 
@@ -551,13 +551,14 @@ size_t sort_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
                               (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 64);
-    return bytes;
+    return std::max(bytes, slot_sort_temp_bytes(n, 8));
 }
 
 hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit) {
     if (b.n == 0) return hipSuccess;
     size_t bytes = b.sort_tmp_bytes;
     // Morton keys use bits [0, 63), the centroid hash bits [0, 32); invalid beams sort last either way.
+    if (b.slot) return slot_sort_pairs(b.sort_tmp, b.keys, b.keys_alt, b.vals, b.vals_alt, b.n, 0, end_bit, s);
     return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n, 0,
                                      (unsigned int)end_bit, s);
 }
@@ -592,7 +593,7 @@ hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s
                        b.leaf_parent);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(b.visit, 0, sizeof(unsigned int) * (size_t)(nleaf - 1), s);
+    e = b.slot ? slot_fill(b.visit, nleaf - 1, 0u, s) : hipMemsetAsync(b.visit, 0, sizeof(unsigned int) * (size_t)(nleaf - 1), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_refit, dim3(grid_for(nleaf)), dim3(kBlock), 0, s, b.recs, nvalid, K, nleaf, b.nodes,
                        b.leaf_parent, b.visit);

@@ -391,7 +391,7 @@ __device__ void estimate_direct(const DevScene &S, HaltonDev &hs, f3 p, f3 perr,
     }
 }
 
-__global__ __launch_bounds__(kCamBlock) void k_camera(const DevScene *__restrict__ Sp, const DevCamera *__restrict__ Cp,
+__global__ __launch_bounds__(kCamBlock, 6) void k_camera(const DevScene *__restrict__ Sp, const DevCamera *__restrict__ Cp,
                                                      const uint16_t *__restrict__ perms, int iteration, int max_depth,
                                                      int render_surfaces, int render_media, int64_t nslots,
                                                      float *__restrict__ so, float *__restrict__ sp_,
@@ -546,13 +546,14 @@ size_t camera_scan_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::exclusive_scan(nullptr, bytes, (const int32_t *)nullptr, (int64_t *)nullptr, int64_t(0),
                                   (size_t)n, rocprim::plus<int64_t>());
-    return bytes;
+    return std::max(bytes, slot_scan_temp_bytes(n));
 }
 
 hipError_t launch_camera_scan(void *tmp, size_t tmp_bytes, const CamSlots &s, int64_t nslots, int max_depth,
-                              int64_t *offs, hipStream_t stream) {
+                              int64_t *offs, hipStream_t stream, bool slot) {
     const int64_t total = nslots * max_depth;
     if (total == 0) return hipSuccess;
+    if (slot) return slot_exclusive_scan(s.valid, offs, total, nullptr, tmp, stream);  // one-wave (bre_slot.hip)
     return rocprim::exclusive_scan(tmp, tmp_bytes, s.valid, offs, int64_t(0), (size_t)total, rocprim::plus<int64_t>(),
                                    stream);
 }
@@ -561,8 +562,8 @@ hipError_t launch_camera_compact(const CamSlots &s, int64_t nslots, int max_dept
                                  float *p, float *d, float *t, int32_t *pix, int32_t *depth, hipStream_t stream) {
     const int64_t total = nslots * max_depth;
     if (total == 0) return hipSuccess;
-    const unsigned blocks = (unsigned)((total + 255) / 256);
-    hipLaunchKernelGGL(k_compact, dim3(blocks), dim3(256), 0, stream, total, s.valid, offs, s.o, s.p, s.d, s.t,
+    const unsigned blocks = (unsigned)((total + 63) / 64);  // one-wave workgroups (bre_slot.hip)
+    hipLaunchKernelGGL(k_compact, dim3(blocks), dim3(64), 0, stream, total, s.valid, offs, s.o, s.p, s.d, s.t,
                        s.pix, o, p, d, t, pix, depth, nslots);
     return hipGetLastError();
 }

@@ -93,6 +93,7 @@ struct BuildBuffers {
     float *gbox;            // 6n (input order): equal-centroid group boxes (tree key 1)
     unsigned int *nvalid;   // 3: valid beams, then the ordered min and max of their radii
     int uniform_radius = 0; // k_pack: the set's BeamSet::uniform (read back after k_prep)
+    int slot = 1;           // sorts and fills by the one-wave primitives (bre_slot.hip), 0: rocPRIM / hipMemset
     unsigned long long *keys, *keys_alt;
     int32_t *vals, *vals_alt;
     void *sort_tmp;
@@ -193,6 +194,8 @@ struct GatherArgs {
     int margin;            // tile kernel prefilter margins: 1 = the tight bound (default), 0 = round 2's
     TileAxis *tileax;      // tile kernel: per-tile axis bounds (ntiles), null = no tile axis reject
     unsigned int *segbox;  // tile kernel: 6 ordered uints of scratch (the launch's segment box)
+    hipEvent_t wait_ev = nullptr;  // tile kernel: the stream waits for it right before the launch (null: no wait)
+    hipEvent_t done_ev = nullptr;  // tile kernel: recorded right after the launch (null: none)
 };
 
 // capsule-chunk index (bre_chunk.hip)
@@ -257,6 +260,7 @@ struct SegSort {
     int key_mode;  // 0: Morton of (origin, octahedral direction); 1: Morton of (origin, end point);
                    // 2 / 3: the segment's line (dominant-axis class + slopes + plane crossing [+ midpoint]);
                    // 4: Hilbert order of (origin, end point) (the default, bre_math.h hilbert_key)
+    int slot = 1;  // the sort by the one-wave radix sort (bre_slot.hip), 0: rocPRIM
 };
 size_t seg_sort_temp_bytes(int64_t n);
 // deterministic per-pixel accumulation of per-segment sums (bre_sort.hip): stable sort of the
@@ -275,12 +279,15 @@ struct PixelCompose {
     size_t tmp_bytes;
     unsigned int *flags;     // DevCounters::flags
     unsigned int bad_pixel_flag;
+    int slot = 1;            // the sort by the one-wave radix sort (bre_slot.hip), 0: rocPRIM
 };
 size_t pixel_sort_temp_bytes(int64_t n);
 hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st);
 // film class of each caller-order segment: chunk (sorted position / 64 / block) mod classes; perm[i] =
 // the caller index of sorted segment i (nullptr: unsorted, the caller's order)
 hipError_t launch_seg_classes(int64_t n, int block, int classes, const int32_t *perm, uint8_t *cls, hipStream_t st);
+// dst[i] += src[i] for i < m, then src[i] = 0 if clear (one-wave workgroups)
+hipError_t launch_film_add(int64_t m, float *src, float *dst, int clear, hipStream_t st);
 // out[i] = sum over the classes of in[c][i] in class order, i < m
 hipError_t launch_resolve_classes(int64_t m, int classes, const float *in, float *out, hipStream_t st);
 
@@ -293,8 +300,22 @@ hipError_t launch_packet_pick(int64_t n, int64_t m, int rank, int count, int chu
 hipError_t launch_device_check(int kind, int64_t n, const float *x, int n_aux, const float *aux, float *y,
                                hipStream_t s);
 
+// one-wave pass primitives (bre_slot.hip): every kernel in 64-thread workgroups with <= 1 KB of LDS, so
+// that a concurrent gather's retiring one-wave slots take them (the pipelined pass chain)
+hipError_t slot_fill(void *p, int64_t nwords, unsigned int value, hipStream_t s);
+size_t slot_scan_temp_bytes(int64_t n);
+// out[i] = in[0] + ... + in[i-1] for i < n; *total (may be null) = the whole sum
+hipError_t slot_exclusive_scan(const int32_t *in, int64_t *out, int64_t n, int64_t *total, void *tmp, hipStream_t s);
+size_t slot_sort_temp_bytes(int64_t n, int key_bytes);
+// stable LSD radix sort of (k0, v0) by key bits [begin_bit, end_bit) into (k1, v1); (k0, v0) unchanged
+hipError_t slot_sort_pairs(void *tmp, const unsigned long long *k0, unsigned long long *k1, const int32_t *v0,
+                           int32_t *v1, int64_t n, int begin_bit, int end_bit, hipStream_t s);
+hipError_t slot_sort_pairs(void *tmp, const unsigned int *k0, unsigned int *k1, const int32_t *v0, int32_t *v1,
+                           int64_t n, int begin_bit, int end_bit, hipStream_t s);
+
 // gather kernels (bre_gather.hip)
-hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s);
+size_t roots_scratch_bytes();
+hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, void *scratch, hipStream_t s);
 hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipStream_t s);
 hipError_t launch_roots_shard(const int32_t *roots, int S, int rank, int count, int S2, int32_t *out,
                               hipStream_t s);

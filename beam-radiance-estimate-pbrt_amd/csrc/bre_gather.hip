@@ -34,24 +34,11 @@ namespace {
 
 constexpr int kThreadBlock = 128;  // 2 waves, 32 KiB LDS stack
 
-// Profiling ablations (compile-time, off in the product; profiles/variant.sh builds them into
-// separate libraries): BRE_ABLATE 2 = no exact stage (queue drained unread), 3 = no prefilter scan
-// (every kept beam's prefilter replaced by a fixed 1-in-8 lane pattern), 4 = traversal only (leaf
-// tiles not scanned), 5 = exact stage accumulates in one racy RMW round instead of the ordered rank
-// rounds (wrong sums: the price of the ordering).  The variants measured negative in rounds 2-4 (the
-// binary walk, node reload / prefetch, segment values by ds_bpermute, round 3's ranks and LDS float
-// atomics past 8 rounds, the box reject off, pointer loads of SegRec and of the unit direction) were
-// removed in round 5: profiles/r5/negative/ablation_switches.patch restores them.
-#ifndef BRE_ABLATE
-#define BRE_ABLATE 0
-#endif
-// BRE_NO_QCOUNT / BRE_NO_TAX (timing A/B only): compile out the production queue count / the tile line reject
-#ifndef BRE_NO_QCOUNT
-#define BRE_NO_QCOUNT 0
-#endif
-#ifndef BRE_NO_TAX
-#define BRE_NO_TAX 0
-#endif
+// The timing ablations of rounds 2-5 (BRE_ABLATE 2-5: no exact stage, no prefilter scan, traversal
+// only, one racy accumulation round; BRE_NO_QCOUNT / BRE_NO_TAX) are not in the production source since
+// round 6: profiles/r6/negative/ablation_switches_r6.patch restores them (and
+// profiles/r5/negative/ablation_switches.patch the variants measured negative in rounds 2-4).  The two
+// profiling builds below stay: profiles/phase_timing.py and profiles/scan_stats.py use them.
 // BRE_PHASE_TIMING 1 (profiling builds only): the production tile kernel adds, per wave, the
 // shader-clock cycles (s_memtime) of its phases into the counter block -- leaf staging into
 // `candidates`, the prefilter scan into `contributions`, the exact stage into `node_visits`, the
@@ -375,12 +362,15 @@ __global__ void k_segbox_init(unsigned int *__restrict__ b) {
 // box of the launch's finite segment end points (6 ordered uints: min xyz, max xyz).  Grid-stride
 // over a bounded grid, reduced per wave and then per block in LDS: one set of six atomics per block
 // (per-wave atomics on the same six words serialised at the L2: 0.64 ms at C2's 0.6M segments)
-constexpr int kSegboxBlocks = 256;
-__global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__restrict__ o, const float *__restrict__ p,
+constexpr int kSegboxBlocks = 512;
+// the kernels around the gather run in one-wave workgroups (bre_slot.hip: they then fit the slots a
+// concurrent gather's retiring waves free, so the pipelined pass chain runs inside the other gather)
+constexpr int kPassBlock = 64;
+__global__ __launch_bounds__(kPassBlock) void k_segbox(int64_t nseg, const float *__restrict__ o, const float *__restrict__ p,
                                                 unsigned int *__restrict__ b) {
-    __shared__ unsigned int red[4][6];
+    __shared__ unsigned int red[kPassBlock / 64][6];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * 256) {
+    for (int64_t i = (int64_t)blockIdx.x * kPassBlock + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * kPassBlock) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const float *q = (e ? p : o) + 3 * i;
@@ -414,7 +404,7 @@ __global__ __launch_bounds__(256) void k_segbox(int64_t nseg, const float *__res
     if (threadIdx.x < 6) {
         const int k = threadIdx.x;
         unsigned int v = red[0][k];
-        for (int j = 1; j < 4; ++j) v = k < 3 ? min(v, red[j][k]) : max(v, red[j][k]);
+        for (int j = 1; j < kPassBlock / 64; ++j) v = k < 3 ? min(v, red[j][k]) : max(v, red[j][k]);
         if (k < 3)
             atomicMin(&b[k], v);
         else
@@ -788,17 +778,6 @@ __device__ __forceinline__ void tile_exact(TileShared &sh, int first, int n, con
     // instruction are undocumented.  (`count` only decides whether the count is used: it is always kept.)
     (void)count;
     if (__ballot(contrib) == 0ull) return;
-    if (BRE_ABLATE == 5) {  // timing ablation only: one racy read-modify-write round (sums are wrong)
-        if (contrib) {
-            float4 a = sh.acc[sl];
-            a.x += v.x;
-            a.y += v.y;
-            a.z += v.z;
-            a.w += v.w;
-            sh.acc[sl] = a;
-        }
-        return;
-    }
     // rank: every contributing lane ORs its bit into its segment's 64-bit mask with ds_or_rtn_b64, which
     // returns the mask as it was before this lane's OR.  Whatever order the hardware applies one
     // instruction's same-address lanes in, a lane's returned mask holds only lanes of its own segment;
@@ -937,8 +916,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         int h = 0;
         while (t1 - h >= 64) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
-            if (BRE_ABLATE != 2) tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
-            if (!COUNT && !BRE_NO_QCOUNT) pf.queued += 64;  // the production queue's length (counted per batch)
+            tile_exact(sh, h, 64, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
+            if (!COUNT) pf.queued += 64;  // the production queue's length (counted per batch)
             h += 64;
             __builtin_amdgcn_wave_barrier();
         }
@@ -964,8 +943,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             ++pf.leaves;
             pf.beams += nb;
         }
-        if (BRE_ABLATE == 4) return;
-        if (!COUNT && !BRE_NO_TAX && tax != nullptr) {
+        if (!COUNT && tax != nullptr) {
             // the per-lane tile line reject: lanes whose segment line is too far from the tile's axis
             // line leave the tile; a tile no lane keeps is skipped before it is staged
             const float4 *tq = reinterpret_cast<const float4 *>(tax + (int64_t)(~c));
@@ -1091,10 +1069,8 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             if (two) todo &= todo - 1ull;
             const ScanStaged B1 = scan_beam_lds(sh.tile, j1), B2 = scan_beam_lds(sh.tile, j2);
             // lane masks: every lane evaluates both tests, the lanes off the tile are masked out
-            const unsigned long long n1 =
-                (BRE_ABLATE == 3 ? __ballot(((j1 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B1)) & onm;
-            const unsigned long long n2 =
-                (BRE_ABLATE == 3 ? __ballot(((j2 * 7 + lane) & 7) == 0) : scan_keep_mask(SL, L.au, B2)) & onm;
+            const unsigned long long n1 = scan_keep_mask(SL, L.au, B1) & onm;
+            const unsigned long long n2 = scan_keep_mask(SL, L.au, B2) & onm;
             push(n1, (int32_t)(cur_first + j1), lane);
             if (two) push(n2, (int32_t)(cur_first + j2), lane);
             drain();
@@ -1187,7 +1163,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         if (t1 > 0) {
             if (COUNT && lane == 0) ++pf.ccp_waves;
             tile_exact(sh, 0, t1, srec, sd, seg0, recs, pw, bset, R, inv_maxd, count_c, L);
-            if (!COUNT && !BRE_NO_QCOUNT) pf.queued += (unsigned long long)t1;
+            if (!COUNT) pf.queued += (unsigned long long)t1;
         }
         t1 = 0;
     }
@@ -1241,10 +1217,10 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
 // One 64-B record per gathered segment for the tile kernel's exact stage (see SegRec, packet-plane
 // layout): the values load_lane derives, computed once per gather instead of once per (packet,
 // subtree) wave.
-__global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__restrict__ so,
+__global__ __launch_bounds__(kPassBlock) void k_seg_prep(int64_t nseg, const float *__restrict__ so,
                                                   const float *__restrict__ sp_, const float *__restrict__ sd,
                                                   const float *__restrict__ stmax, SegRec *__restrict__ out) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * kPassBlock + threadIdx.x;
     if (s >= nseg) return;
     Lane L;
     load_lane(s, nseg, so, sp_, sd, stmax, L);
@@ -1261,13 +1237,13 @@ __global__ __launch_bounds__(256) void k_seg_prep(int64_t nseg, const float *__r
 // segment's sum to its pixel (one float atomic per channel, PhotonBeamPixel::Ld +=).  With counts,
 // also sum the per-subtree candidate / contribution counts (candidates -1: not counted).  seg_index
 // (optional) maps the gathered order to the caller's order of seg_rgb / seg_counts.
-__global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__restrict__ partial,
+__global__ __launch_bounds__(kPassBlock) void k_reduce(int64_t nseg, const float *__restrict__ partial,
                                                 const int32_t *__restrict__ pcnt, const int32_t *__restrict__ roots,
                                                 int S, const int32_t *__restrict__ pixel, int64_t npix,
                                                 float *__restrict__ accum, float *__restrict__ seg_rgb,
                                                 int32_t *__restrict__ seg_counts, const int32_t *__restrict__ seg_index,
                                                 DevCounters *ctr) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * kPassBlock + threadIdx.x;
     const bool in = s < nseg;
     const int nr = roots[S];
     float cr = 0.f, cg = 0.f, cb = 0.f;
@@ -1348,107 +1324,146 @@ __global__ __launch_bounds__(256) void k_reduce(int64_t nseg, const float *__res
 // ~600 of 4096 slots at S = 256) still yields a valid split: the cached nodes form a subtree from the
 // root, so E's top-(S - 1) choice among them is one too.
 constexpr int kRootSlots = 4096;
-struct RootsShared {
+// the cache, in global scratch (one wave computes the roots: a one-wave workgroup with no LDS fits a
+// concurrent gather's slots, bre_slot.hip; round 5's version kept it in 140 KB of LDS, a whole CU)
+struct RootsScratch {
     int32_t id[kRootSlots];     // cached node
     int32_t nl[kRootSlots];     // its leaf tiles (Node::nleaf)
     int32_t ch[kRootSlots][2];  // its children
     int32_t cw[kRootSlots][2];  // their leaf tiles (1: a leaf tile, 0: empty)
     int32_t cs[kRootSlots][2];  // their cache slots (-1: not cached)
-    unsigned char in_e[kRootSlots];
+    int32_t in_e[kRootSlots];
     int32_t fc[kMaxSplit + 1], fw[kMaxSplit + 1];  // the roots, unordered
-    int cnt, lo, hi, nf;
 };
-// one block holds the whole cache: it must fit gfx950's 160 KB of LDS per CU (k_roots runs as one block)
-static_assert(sizeof(RootsShared) <= 160 * 1024, "k_roots: RootsShared exceeds the 160 KB of LDS of a gfx950 CU");
 
 // children, parent and leaf tiles of node x: the record's last 16 bytes
 __device__ __forceinline__ int4 node_tail(const Node *__restrict__ nodes, int32_t x) {
     return *reinterpret_cast<const int4 *>(&nodes[x].child[0]);
 }
 
-__global__ __launch_bounds__(kMaxSplit) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots) {
-    __shared__ RootsShared sh;
-    if (blockIdx.x != 0) return;
+// the wave's own global writes visible to its later reads (device-scope release + acquire)
+__device__ __forceinline__ void wave_sync_global() {
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+}
+
+// key of a node or root of w leaf tiles and index x: larger first, ties by ascending (signed) index
+__device__ __forceinline__ unsigned long long root_key(int32_t w, int32_t x) {
+    return ((unsigned long long)(unsigned int)w << 32) | (0xffffffffu - ((unsigned int)x ^ 0x80000000u));
+}
+
+// rank of key kk among the n keys key(w[j], x[j]) (the number of larger ones): 64 keys per step, read by
+// one lane each and broadcast by readlane
+__device__ __forceinline__ int rank_among(const int32_t *w, const int32_t *x, int n, unsigned long long kk) {
+    int rank = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + (int)threadIdx.x;
+        const unsigned long long kv = j < n ? root_key(w[j], x[j]) : 0ull;
+        const int m = min(64, n - j0);
+        for (int q = 0; q < m; ++q) {
+            const unsigned long long kj =
+                ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(kv >> 32), q) << 32) |
+                (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)kv, q);
+            rank += kj > kk;
+        }
+    }
+    return rank;
+}
+
+__global__ __launch_bounds__(64) void k_roots(const Node *__restrict__ nodes, int S, int32_t *__restrict__ roots,
+                                              RootsScratch *__restrict__ g) {
     const int t = threadIdx.x;
+    const unsigned long long below = (1ull << t) - 1ull;
     const int32_t total = nodes[0].nleaf;
     const int32_t heavy = total / S;
-    if (t == 0) {
-        sh.id[0] = 0;
-        sh.cnt = 1;
-        sh.lo = 0;
-        sh.hi = 1;
-        sh.nf = 0;
-    }
-    __syncthreads();
-    // 1. breadth-first cache of the heavy interior nodes
-    while (true) {
-        const int a = sh.lo, b = sh.hi;
-        if (a >= b) break;
-        for (int k = a + t; k < b; k += kMaxSplit) {
-            const int4 q = node_tail(nodes, sh.id[k]);
-            sh.nl[k] = q.w;
+    if (t == 0) g->id[0] = 0;
+    wave_sync_global();
+    // 1. breadth-first cache of the heavy interior nodes (slots handed out in lane order per child)
+    int cnt = 1, lo = 0, hi = 1;
+    while (lo < hi) {
+        for (int k0 = lo; k0 < hi; k0 += 64) {
+            const int k = k0 + t;
+            const bool act = k < hi;
+            const int4 q = act ? node_tail(nodes, g->id[k]) : make_int4(kEmptyChild, kEmptyChild, 0, 0);
             const int32_t c[2] = {q.x, q.y};
+            int32_t w[2];
+            bool h[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int32_t w = c[j] == kEmptyChild ? 0 : (c[j] < 0 ? 1 : node_tail(nodes, c[j]).w);
-                int32_t s = -1;
-                if (c[j] >= 0 && w >= heavy) {
-                    s = atomicAdd(&sh.cnt, 1);
-                    if (s < kRootSlots) sh.id[s] = c[j];
-                    else s = -1;
+                w[j] = c[j] == kEmptyChild ? 0 : (c[j] < 0 ? 1 : node_tail(nodes, c[j]).w);
+                h[j] = act && c[j] >= 0 && w[j] >= heavy;
+            }
+            int32_t sl[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const unsigned long long m = __ballot(h[j]);
+                const int s = cnt + __popcll(m & below);
+                sl[j] = (h[j] && s < kRootSlots) ? s : -1;
+                if (sl[j] >= 0) g->id[s] = c[j];
+                cnt += __popcll(m);
+            }
+            if (act) {
+                g->nl[k] = q.w;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    g->ch[k][j] = c[j];
+                    g->cw[k][j] = w[j];
+                    g->cs[k][j] = sl[j];
                 }
-                sh.ch[k][j] = c[j];
-                sh.cw[k][j] = w;
-                sh.cs[k][j] = s;
             }
         }
-        __syncthreads();
-        if (t == 0) {
-            sh.lo = b;
-            sh.hi = min(sh.cnt, kRootSlots);
-        }
-        __syncthreads();
+        wave_sync_global();
+        lo = hi;
+        hi = min(cnt, kRootSlots);
     }
-    const int nc = min(sh.cnt, kRootSlots);
-    const auto key = [](int32_t w, int32_t x) -> unsigned long long {
-        return ((unsigned long long)(unsigned int)w << 32) | (0xffffffffu - ((unsigned int)x ^ 0x80000000u));
-    };
+    const int nc = min(cnt, kRootSlots);
     // 2. E: the S - 1 largest cached nodes
-    for (int k = t; k < nc; k += kMaxSplit) {
-        const unsigned long long kk = key(sh.nl[k], sh.id[k]);
-        int rank = 0;
-        for (int j = 0; j < nc; ++j) rank += key(sh.nl[j], sh.id[j]) > kk;
-        sh.in_e[k] = rank < S - 1;
+    for (int k0 = 0; k0 < nc; k0 += 64) {
+        const int k = k0 + t;
+        const unsigned long long kk = k < nc ? root_key(g->nl[k], g->id[k]) : ~0ull;
+        const int rank = rank_among(g->nl, g->id, nc, kk);
+        if (k < nc) g->in_e[k] = rank < S - 1;
     }
-    __syncthreads();
-    // 3. the roots: E's children outside E
-    for (int k = t; k < nc; k += kMaxSplit) {
-        if (!sh.in_e[k]) continue;
+    wave_sync_global();
+    // 3. the roots: E's children outside E (the whole tree's root when S = 1)
+    int nf = 0;
+    for (int k0 = 0; k0 < nc; k0 += 64) {
+        const int k = k0 + t;
+        const bool e = k < nc && g->in_e[k];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int32_t c = sh.ch[k][j], s = sh.cs[k][j];
-            if (c == kEmptyChild || (s >= 0 && sh.in_e[s])) continue;
-            const int f = atomicAdd(&sh.nf, 1);
-            sh.fc[f] = c;
-            sh.fw[f] = sh.cw[k][j];
+            int32_t c = kEmptyChild, s = -1;
+            if (e) {
+                c = g->ch[k][j];
+                s = g->cs[k][j];
+            }
+            const bool root = e && c != kEmptyChild && !(s >= 0 && g->in_e[s]);
+            const unsigned long long m = __ballot(root);
+            if (root) {
+                const int f = nf + __popcll(m & below);
+                g->fc[f] = c;
+                g->fw[f] = g->cw[k][j];
+            }
+            nf += __popcll(m);
         }
     }
-    if (t == 0 && !sh.in_e[0]) {  // S = 1: the whole tree
-        sh.fc[0] = 0;
-        sh.fw[0] = total;
-        sh.nf = 1;
+    if (!g->in_e[0]) {
+        if (t == 0) {
+            g->fc[0] = 0;
+            g->fw[0] = total;
+        }
+        nf = 1;
     }
-    __syncthreads();
+    wave_sync_global();
     // 4. ranks: leaf tiles descending, ties by child index
-    const int n = sh.nf;
-    if (t < n) {
-        const unsigned long long kk = key(sh.fw[t], sh.fc[t]);
-        int rank = 0;
-        for (int j = 0; j < n; ++j) rank += key(sh.fw[j], sh.fc[j]) > kk;
-        roots[rank] = sh.fc[t];
+    for (int k0 = 0; k0 < nf; k0 += 64) {
+        const int k = k0 + t;
+        const unsigned long long kk = k < nf ? root_key(g->fw[k], g->fc[k]) : ~0ull;
+        const int rank = rank_among(g->fw, g->fc, nf, kk);
+        if (k < nf) roots[rank] = g->fc[k];
     }
-    if (t >= n && t < S) roots[t] = kEmptyChild;
-    if (t == 0) roots[S] = n;
+    for (int k = nf + t; k < S; k += 64) roots[k] = kEmptyChild;
+    if (t == 0) roots[S] = nf;
 }
 
 template <bool COUNT>
@@ -1516,7 +1531,7 @@ __global__ __launch_bounds__(kThreadBlock) void k_gather_thread(
 
 __global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *__restrict__ seg_counts,
                            const int32_t *__restrict__ seg_index) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= nseg) return;
     const int64_t s = seg_index ? (int64_t)seg_index[i] : i;  // the caller's entry of gathered segment i
     if (seg_rgb) {
@@ -1536,9 +1551,9 @@ __global__ void k_zero_seg(int64_t nseg, float *__restrict__ seg_rgb, int32_t *_
 // children, then child 1's), so a fixed-order walk of the 4-wide view visits the leaves in the same
 // left-to-right order as a fixed-order binary walk.  A grandchild box lies inside its parent's box, so
 // testing it directly prunes at least as tightly as testing both levels.
-__global__ __launch_bounds__(256) void k_collapse4(const Node *__restrict__ nodes, int64_t nnodes,
+__global__ __launch_bounds__(64) void k_collapse4(const Node *__restrict__ nodes, int64_t nnodes,
                                                    Node4 *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= nnodes) return;
     const Node &n = nodes[i];
     Node4 q;
@@ -1574,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_collapse4(const Node *__restrict__ node
 
 hipError_t launch_collapse4(const Node *nodes, int64_t nnodes, Node4 *out, hipStream_t s) {
     if (nnodes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_collapse4, dim3((unsigned int)((nnodes + 255) / 256)), dim3(256), 0, s, nodes, nnodes, out);
+    hipLaunchKernelGGL(k_collapse4, dim3((unsigned int)((nnodes + 63) / 64)), dim3(64), 0, s, nodes, nnodes, out);
     return hipGetLastError();
 }
 
@@ -1590,12 +1605,14 @@ __global__ void k_roots_shard(const int32_t *__restrict__ roots, int S, int rank
 
 hipError_t launch_roots_shard(const int32_t *roots, int S, int rank, int count, int S2, int32_t *out,
                               hipStream_t s) {
-    hipLaunchKernelGGL(k_roots_shard, dim3(1), dim3(256), 0, s, roots, S, rank, count, S2, out);
+    hipLaunchKernelGGL(k_roots_shard, dim3(1), dim3(64), 0, s, roots, S, rank, count, S2, out);
     return hipGetLastError();
 }
 
-hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, hipStream_t s) {
-    hipLaunchKernelGGL(k_roots, dim3(1), dim3(kMaxSplit), 0, s, nodes, S, roots);
+size_t roots_scratch_bytes() { return sizeof(RootsScratch); }
+
+hipError_t launch_roots(const Node *nodes, int S, int32_t *roots, void *scratch, hipStream_t s) {
+    hipLaunchKernelGGL(k_roots, dim3(1), dim3(64), 0, s, nodes, S, roots, static_cast<RootsScratch *>(scratch));
     return hipGetLastError();
 }
 
@@ -1624,13 +1641,13 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     if ((counters || a.seg_counts) && !pcnt) return hipErrorInvalidValue;
     if (!a.segrec || a.leaf_size > 64) return hipErrorInvalidValue;
     if (!a.nodes4) return hipErrorInvalidValue;  // the 4-wide walk needs the collapsed view
-    hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p, a.d,
+    hipLaunchKernelGGL(k_seg_prep, dim3((unsigned int)((a.nseg + kPassBlock - 1) / kPassBlock)), dim3(kPassBlock), 0, s, a.nseg, a.o, a.p, a.d,
                        a.tmax, a.segrec);
     const TileAxis *tax = nullptr;
     if (a.tileax && a.segbox && a.prefilter && a.nvalid > 0) {
         const int64_t ntiles = (a.nvalid + a.leaf_size - 1) / a.leaf_size;
         hipLaunchKernelGGL(k_segbox_init, dim3(1), dim3(64), 0, s, a.segbox);
-        hipLaunchKernelGGL(k_segbox, dim3((unsigned int)std::min<int64_t>(kSegboxBlocks, (a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.o, a.p,
+        hipLaunchKernelGGL(k_segbox, dim3((unsigned int)std::min<int64_t>(kSegboxBlocks, (a.nseg + kPassBlock - 1) / kPassBlock)), dim3(kPassBlock), 0, s, a.nseg, a.o, a.p,
                            a.segbox);
         hipLaunchKernelGGL(k_tile_axis, dim3((unsigned int)ntiles), dim3(64), 0, s, a.recs, a.bset, a.nvalid,
                            a.leaf_size, a.segbox, a.R, a.tileax);
@@ -1641,6 +1658,10 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     // ceil(S / count)) would leave roots unassigned, so such launches take the LPT map
     GatherArgs am = a;
     if (am.block_map == 0 && (am.split & 7) != 0) am.block_map = 3;
+    if (a.wait_ev) {  // another context's tile kernel first (bre_set_gather_after)
+        const hipError_t ew = hipStreamWaitEvent(s, a.wait_ev, 0);
+        if (ew != hipSuccess) return ew;
+    }
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nodes4, a.nvalid,        \
@@ -1664,14 +1685,18 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
 #undef BRE_LAUNCH_TILE
     hipError_t e4 = hipGetLastError();
     if (e4 != hipSuccess) return e4;
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.partial, pcnt,
+    if (a.done_ev) {
+        e4 = hipEventRecord(a.done_ev, s);
+        if (e4 != hipSuccess) return e4;
+    }
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + kPassBlock - 1) / kPassBlock)), dim3(kPassBlock), 0, s, a.nseg, a.partial, pcnt,
                        a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb, a.seg_counts, a.seg_index, a.ctr);
     return hipGetLastError();
 }
 
 hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s) {
     if (a.nseg == 0 || (!a.seg_rgb && !a.seg_counts)) return hipSuccess;
-    hipLaunchKernelGGL(k_zero_seg, dim3((unsigned int)((a.nseg + 255) / 256)), dim3(256), 0, s, a.nseg, a.seg_rgb,
+    hipLaunchKernelGGL(k_zero_seg, dim3((unsigned int)((a.nseg + 63) / 64)), dim3(64), 0, s, a.nseg, a.seg_rgb,
                        a.seg_counts, a.seg_index);
     return hipGetLastError();
 }

@@ -119,7 +119,7 @@ void prepare_scene(const bre_scene *s, HostScene *out, const float *d_density) {
 namespace {
 
 #ifndef BRE_PHOTON_BLOCK
-#define BRE_PHOTON_BLOCK 128
+#define BRE_PHOTON_BLOCK 64  // one wave: fits a concurrent gather's slots (bre_slot.hip; 128 until round 5)
 #endif
 constexpr int kPhotonBlock = BRE_PHOTON_BLOCK;
 
@@ -137,7 +137,7 @@ struct Frame {
 // whose count exceeds `over`, the single-trace form's overflow); 2: write the first `over` beams to
 // the photon's slots i * over + k and count them all.
 template <int MODE>
-__global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__restrict__ Sp, int64_t n, uint64_t seq0,
+__global__ __launch_bounds__(kPhotonBlock, 6) void k_photons(const DevScene *__restrict__ Sp, int64_t n, uint64_t seq0,
                                                           int max_depth, float radius, int32_t *__restrict__ counts,
                                                           const int64_t *__restrict__ offsets, float *__restrict__ bs,
                                                           float *__restrict__ be, float *__restrict__ br,
@@ -300,16 +300,17 @@ __global__ __launch_bounds__(kPhotonBlock) void k_photons(const DevScene *__rest
 // Each wave copies the beams of its 64 photons as one run: lane j takes the wave's j-th beam (owner by
 // a search of the wave's prefix sums in LDS), so the writes of consecutive lanes are consecutive and a
 // photon's slots are read together (a thread per photon strided its reads by cap slots: 0.27 ms at C2).
-__global__ __launch_bounds__(256) void k_photon_slots(int64_t n, int cap, const int32_t *__restrict__ counts,
+constexpr int kSlotsBlock = 64;
+__global__ __launch_bounds__(kSlotsBlock) void k_photon_slots(int64_t n, int cap, const int32_t *__restrict__ counts,
                                                       const int64_t *__restrict__ offsets, const float *__restrict__ ss,
                                                       const float *__restrict__ se, const float *__restrict__ sr,
                                                       const float *__restrict__ sp, float *__restrict__ bs,
                                                       float *__restrict__ be, float *__restrict__ br,
                                                       float *__restrict__ bp) {
-    __shared__ int pre[4][65];      // per wave: exclusive prefix sums of the photons' copied beams
-    __shared__ int64_t off[4][64];  // per wave: the photons' output offsets
+    __shared__ int pre[kSlotsBlock / 64][65];      // per wave: exclusive prefix sums of the photons' copied beams
+    __shared__ int64_t off[kSlotsBlock / 64][64];  // per wave: the photons' output offsets
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kSlotsBlock + threadIdx.x;
     const int64_t i0 = i - lane;
     const int m = i < n ? min(counts[i], cap) : 0;
     int incl = m;
@@ -368,7 +369,7 @@ hipError_t launch_photon_slots(int64_t n, int cap, const int32_t *counts, const 
                                const float *se, const float *sr, const float *sp, float *start, float *end,
                                float *rad, float *power, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_photon_slots, dim3((unsigned int)((n + 255) / 256)), dim3(256), 0, s, n, cap, counts, offsets,
+    hipLaunchKernelGGL(k_photon_slots, dim3((unsigned int)((n + kSlotsBlock - 1) / kSlotsBlock)), dim3(kSlotsBlock), 0, s, n, cap, counts, offsets,
                        ss, se, sr, sp, start, end, rad, power);
     return hipGetLastError();
 }
@@ -377,12 +378,13 @@ size_t count_scan_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::inclusive_scan(nullptr, bytes, (const int32_t *)nullptr, (int64_t *)nullptr, (size_t)n,
                                   rocprim::plus<int64_t>());
-    return bytes;
+    return std::max(bytes, slot_scan_temp_bytes(n));
 }
 
-// offsets[0] = 0, offsets[k + 1] = counts[0] + ... + counts[k]
+// offsets[0] = 0, offsets[k + 1] = counts[0] + ... + counts[k].  slot: the one-wave scan (bre_slot.hip)
 hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n,
-                             hipStream_t s) {
+                             hipStream_t s, bool slot) {
+    if (slot) return slot_exclusive_scan(counts, offsets, n, offsets + n, tmp, s);
     hipError_t e = hipMemsetAsync(offsets, 0, sizeof(int64_t), s);
     if (e != hipSuccess || n == 0) return e;
     return rocprim::inclusive_scan(tmp, bytes, counts, offsets + 1, (size_t)n, rocprim::plus<int64_t>(), s);

@@ -12,6 +12,8 @@
 // at C2 shortens the gather by ~5% over the (origin, direction) key (mode 0).  Only the order changes; every per-segment sum and every
 // pixel total is the same set of pair contributions.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <float.h>
@@ -24,7 +26,7 @@ namespace bre {
 namespace {
 
 #ifndef BRE_PASS_BLOCK
-#define BRE_PASS_BLOCK 256
+#define BRE_PASS_BLOCK 64  // one wave (bre_slot.hip; 256 until round 5)
 #endif
 constexpr int kBlock = BRE_PASS_BLOCK;  // threads per block of the pass kernels
 
@@ -361,7 +363,22 @@ __global__ __launch_bounds__(kBlock) void k_resolve_classes(int64_t m, int class
     out[i] = v;
 }
 
+// dst += src (element-wise, a film of one iteration into the render's film), then src = 0 when asked
+__global__ __launch_bounds__(kBlock) void k_film_add(int64_t m, float *src, float *__restrict__ dst, int clear) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
+        dst[i] += src[i];
+        if (clear) src[i] = 0.f;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_film_add(int64_t m, float *src, float *dst, int clear, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    const int64_t g = (m + 4 * kBlock - 1) / (4 * kBlock);
+    hipLaunchKernelGGL(k_film_add, dim3((unsigned)std::min<int64_t>(g, 1 << 20)), dim3(kBlock), 0, st, m, src, dst, clear);
+    return hipGetLastError();
+}
 
 hipError_t launch_seg_classes(int64_t n, int block, int classes, const int32_t *perm, uint8_t *cls, hipStream_t st) {
     if (n <= 0) return hipSuccess;
@@ -389,7 +406,7 @@ size_t seg_sort_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                     (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 64);  // the widest key any mode sorts
-    return bytes;
+    return std::max(bytes, slot_sort_temp_bytes(n, 8));
 }
 
 hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
@@ -416,7 +433,8 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.tmp_bytes;
-    e = rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, key_bits, st);
+    e = s.slot ? slot_sort_pairs(s.tmp, s.keys, s.keys_alt, s.vals, s.vals_alt, s.n, 0, key_bits, st)
+               : rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
                        s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);
@@ -427,7 +445,7 @@ size_t pixel_sort_temp_bytes(int64_t n) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned int *)nullptr, (unsigned int *)nullptr,
                                     (int32_t *)nullptr, (int32_t *)nullptr, (size_t)n, 0, 32);
-    return bytes;
+    return std::max(bytes, slot_sort_temp_bytes(n, 4));
 }
 
 hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st) {
@@ -440,7 +458,8 @@ hipError_t launch_pixel_compose(const PixelCompose &c, hipStream_t st) {
     int bits = 1;
     while (bits < 32 && ((uint64_t)1 << bits) < top) ++bits;
     size_t bytes = c.tmp_bytes;
-    e = rocprim::radix_sort_pairs(c.tmp, bytes, c.keys, c.keys_alt, c.vals, c.vals_alt, (size_t)c.n, 0, bits, st);
+    e = c.slot ? slot_sort_pairs(c.tmp, c.keys, c.keys_alt, c.vals, c.vals_alt, c.n, 0, bits, st)
+               : rocprim::radix_sort_pairs(c.tmp, bytes, c.keys, c.keys_alt, c.vals, c.vals_alt, (size_t)c.n, 0, bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pix_compose, dim3(grid_of(c.n)), dim3(kBlock), 0, st, c.n, c.keys_alt, c.vals_alt, c.seg_rgb,
                        c.npix, c.accum, c.flags, c.bad_pixel_flag);

@@ -565,7 +565,7 @@ hipError_t launch_camera(const DevScene *scene, int stack_depth, const DevCamera
                          int shard_block, int classes, hipStream_t stream);
 size_t camera_scan_temp_bytes(int64_t n);
 hipError_t launch_camera_scan(void *tmp, size_t tmp_bytes, const CamSlots &s, int64_t nslots, int max_depth,
-                              int64_t *offs, hipStream_t stream);
+                              int64_t *offs, hipStream_t stream, bool slot);
 hipError_t launch_camera_compact(const CamSlots &s, int64_t nslots, int max_depth, const int64_t *offs, float *o,
                                  float *p, float *d, float *t, int32_t *pix, int32_t *depth, hipStream_t stream);
 
@@ -585,7 +585,7 @@ hipError_t launch_photon_slots(int64_t n, int cap, const int32_t *counts, const 
                                const float *se, const float *sr, const float *sp, float *start, float *end,
                                float *rad, float *power, hipStream_t s);
 size_t count_scan_temp_bytes(int64_t n);
-hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n,
-                             hipStream_t s);
+hipError_t launch_count_scan(void *tmp, size_t bytes, const int32_t *counts, int64_t *offsets, int64_t n, hipStream_t s,
+                             bool slot);
 
 }  // namespace bre

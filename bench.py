@@ -100,6 +100,8 @@ def parse(argv=None):
     ap.add_argument("--photon-single", type=int, default=-1, help=argparse.SUPPRESS)  # photon pass form A/B (option 116)
     ap.add_argument("--pass-priority", type=int, default=-1, help=argparse.SUPPRESS)  # option 117 A/B
     ap.add_argument("--partial-mib", type=int, default=-1, help=argparse.SUPPRESS)  # option 109: launches per gather
+    ap.add_argument("--readback", type=int, default=-1, help=argparse.SUPPRESS)  # option 118 A/B
+    ap.add_argument("--slot-passes", type=int, default=-1, help=argparse.SUPPRESS)  # option 119 A/B
     ap.add_argument("--film-classes", type=int, default=1,
                     help="packet shards: keep the film as 8 packet-class planes, gathered and resolved in class "
                          "order, so every N dividing 8 renders the one-GPU film bit for bit (0: one film, "
@@ -107,6 +109,9 @@ def parse(argv=None):
     ap.add_argument("--pipeline", type=int, default=1,
                     help="scenes: two libbre contexts on two streams, iteration k+1's photon pass / build / "
                          "camera pass overlapping iteration k's gather (0: one context)")
+    ap.add_argument("--gather-fence", type=int, default=1,
+                    help="pipelined contexts: 1 = a context's tile kernel waits for the other's last one "
+                         "(bre_set_gather_after), 0 = the two gathers may interleave")
     ap.add_argument("--shard-mode", choices=["packets", "tiles", "roots"], default="packets",
                     help="strong scaling: each GPU gathers a range of the sorted segment packets (default) "
                          "or owns image tiles")
@@ -129,9 +134,11 @@ def parse(argv=None):
                          "threads, each pixel's depths in order) through bre_gather_device, the C-ABI entry the "
                          "pbrt adapter uses")
     ap.add_argument("--no-legs", action="store_true",
-                    help="c2: skip the untimed-by-headline C3 (N=1) and C4 (every N) iteration-0 legs")
+                    help="c2: skip the untimed-by-headline C3 (N=1), C4 and C5 (every N) legs")
     ap.add_argument("--c4-leg", choices=["auto", "on", "off"], default="auto",
                     help="c2: the C4 iteration-0 gather leg (auto: with strong scaling, at every N)")
+    ap.add_argument("--c5-leg", choices=["auto", "on", "off"], default="auto",
+                    help="c2: the C5 last-pass (iteration 9) gather leg (auto: with strong scaling, at every N)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--progress", action="store_true",
                     help="print a line per timed step to stderr (synchronises each step; long C4/C5 runs)")
@@ -226,6 +233,11 @@ def main():
         # --pipeline 1: a second context on a second stream, iterations alternating between them, so
         # iteration k+1's photon pass, BVH build and camera pass overlap iteration k's gather
         extra = [make_ctx()] if (args.pipeline and not args.pmc_child) else []
+        if extra and args.gather_fence:
+            # the two contexts' tile kernels back to back (bre_set_gather_after): each context's passes and
+            # segment sort run inside the other's gather, but the gathers do not interleave
+            extra[0][0].set_gather_after(g)
+            g.set_gather_after(extra[0][0])
         wl = SceneWorkload(args, bre, [(g, stream)] + extra, frame, srank, scount)
     else:
         wl = SyntheticWorkload(args, bre, g, frame, dev)
@@ -348,6 +360,9 @@ def main():
             legs["c3"] = config_leg(args, bre, dmod, dev, "c3", 1, 0)
         if args.c4_leg == "on" or (args.c4_leg == "auto" and args.scaling == "strong"):
             legs["c4"] = config_leg(args, bre, dmod, dev, "c4", world, rank)
+        if args.c5_leg == "on" or (args.c5_leg == "auto" and args.scaling == "strong"):
+            # C5's last progressive pass (iteration 9: the smallest radius of its ten)
+            legs["c5"] = config_leg(args, bre, dmod, dev, "c5", world, rank, iteration=9)
         if rank == 0:
             result["config_legs"] = legs
     if rank == 0:
@@ -384,12 +399,14 @@ def late_step(wl, steps):
     return max(range(steps), key=lambda k: (wl.iteration(k), -k))
 
 
-def config_leg(args, bre, dmod, dev, name, world, rank):
-    """One iteration (iteration 0, the largest radius) of BASELINE configuration `name` on a fresh
-    context: photon pass + build, camera pass, and the gather of this rank's share of the sorted segment
-    packets, the gather timed by HIP events on its stream.  With N ranks: the gather time is the max over
-    ranks, the estimates their sum, and the partial films are reduced to rank 0 (one RCCL reduce).
-    Errors are reported in the leg, never raised (the headline line stands on its own)."""
+def config_leg(args, bre, dmod, dev, name, world, rank, iteration=0):
+    """One iteration of BASELINE configuration `name` on a fresh context (iteration 0, the largest radius,
+    for C3 / C4; C5's last pass, iteration 9, the smallest radius of its progressive schedule): photon
+    pass + build, camera pass, and the gather of this rank's share of the sorted segment packets, the
+    gather timed by HIP events on its stream.  With N ranks: the gather time is the max over ranks (every
+    rank's time is listed too), the estimates their sum, and the ranks' packet-class film planes are
+    gathered to rank 0, whose film digest must not depend on N (the one-GPU film bit for bit).  Errors
+    are reported in the leg, never raised (the headline line stands on its own)."""
     import argparse as ap_
     import torch
     import torch.distributed as dist
@@ -408,32 +425,40 @@ def config_leg(args, bre, dmod, dev, name, world, rank):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        n = wl.step(0, ev, scratch=False)
+        n = wl.step(iteration, ev, scratch=False)
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         gms = ev[0].elapsed_time(ev[1])
         nb = int(wl.nbeams)
+        per_rank, n_ranks = [gms], 1
         if world > 1:
             cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-            tt = torch.tensor([gms, wall], dtype=torch.float64, device=cdev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            gms, wall = float(tt[0]), float(tt[1])
-            tot = torch.tensor([n], dtype=torch.int64, device=cdev)
-            dist.all_reduce(tot)
-            n_all = int(tot.item())
+            mine = torch.tensor([gms, wall, float(n)], dtype=torch.float64, device=cdev)
+            parts = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            per_rank = [float(p[0]) for p in parts]
+            gms, wall = max(per_rank), max(float(p[1]) for p in parts)
+            n_all = int(sum(float(p[2]) for p in parts))
+            n_ranks = dist.get_world_size()
             frame.gather_to_root(0)
             torch.cuda.synchronize(dev)
         else:
             n_all = n
+        digest = film_digest(frame) if rank == 0 else None
         wl.close()
         c.close()
-        return {"workload": f"{name.upper()} iteration 0 ({preset['photons'] / 1e6:g}M photons, {a.width}x{a.height}, "
-                            f"{'grid-density smoke, g 0.7' if preset['medium'] == 'smoke' else 'homogeneous fog'})",
-                "n_gpus": world, "estimates": n_all, "beams": nb,
-                "gather_ms": gms, "gather_estimates_per_s": n_all / (gms * 1e-3),
+        it = wl.iteration(iteration)
+        return {"workload": f"{name.upper()} iteration {it} ({preset['photons'] / 1e6:g}M photons, {a.width}x{a.height}, "
+                            f"{'grid-density smoke, g 0.7' if preset['medium'] == 'smoke' else 'homogeneous fog'}, "
+                            f"R {wl.radius(it):.6g})",
+                "iteration": it, "n_gpus": world, "ranks_live": n_ranks, "estimates": n_all, "beams": nb,
+                "gather_ms": gms, "gather_ms_per_rank": per_rank, "gather_estimates_per_s": n_all / (gms * 1e-3),
                 "iteration_ms": wall * 1e3, "iteration_estimates_per_s": n_all / wall,
-                "timing": "gather: HIP events around the tile kernel launch on its stream, max over ranks; "
-                          "iteration: wall time of photon pass + build + camera pass + gather, max over ranks"}
+                "film_digest": digest,
+                "timing": "gather: HIP events around the tile kernel launch on its stream, max over ranks (each "
+                          "rank's in gather_ms_per_rank); iteration: wall time of photon pass + build + camera pass "
+                          "+ gather, max over ranks; film_digest: the root's film after the plane gather (the same "
+                          "for every N dividing 8)"}
     except Exception as e:  # reported, never fatal to the headline line
         return {"error": f"{type(e).__name__}: {e}"}
 
@@ -453,7 +478,7 @@ def make_context(bre, args, dev):
                      (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
                      (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose),
                      (116, args.photon_single), (117, args.pass_priority),
-                     (109, args.partial_mib)):
+                     (109, args.partial_mib), (118, args.readback), (119, args.slot_passes)):
         if val >= 0:
             c.set_option(opt, val)
     if film_classes(args) > 1:
@@ -738,7 +763,9 @@ class SceneWorkload:
         R = self.radius(it)
         rec = self.recorder_segments(it) if a.entry == "boundary" else None
         with torch.cuda.stream(st):
-            ld.zero_()
+            # ld is zero here: it starts zeroed and the film add below clears it (a framework zero_ / add_
+            # would queue multi-wave kernels that wait behind the other context's gather; bre_film_add's
+            # one-wave kernel runs beside it, bre_slot.hip)
             self.nbeams = g.trace_photons(self.scene, a.photons, it, a.max_depth, R)  # photon pass + BVH build
             if rec is None:
                 n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
@@ -754,7 +781,7 @@ class SceneWorkload:
                 ev[1].record()
             if self._last_add is not None:
                 st.wait_event(self._last_add)
-            film.add_(ld)
+            g.film_add(ld, film, clear_src=True)  # film += ld; ld = 0
             self._last_add = torch.cuda.Event()
             self._last_add.record(st)
         if self.args.shard_mode == "roots" and self.shard[1] > 1:  # every segment, 1/count of the subtrees
@@ -774,6 +801,9 @@ class SceneWorkload:
             torch.cuda.current_stream().wait_event(self._last_add)
 
     def close(self):
+        for c, _ in self.ctxs:  # unlink the pipelined contexts (bre_set_gather_after) before any is destroyed
+            if getattr(c, "_after", None) is not None:
+                c.set_gather_after(None)
         for c, _ in self.ctxs[1:]:
             c.close()
 

@@ -220,6 +220,21 @@ bre_status bre_gather_device(bre_ctx *ctx, int64_t nseg, const float *d_seg_o_xy
    out may alias classes[0]. */
 bre_status bre_resolve_classes(bre_ctx *ctx, int64_t npix, const float *d_classes, float *d_out);
 
+/* The render's film over iterations: d_dst[i] += d_src[i] for the n_floats floats i, then d_src[i] = 0
+   when clear_src is nonzero (device pointers, distinct; asynchronous on the context's stream).  The
+   reference adds every iteration into the same PhotonBeamPixel::Ld (photonbeam.cpp:477-504, 578); a
+   caller that renders each iteration into its own image (bench.py's pipelined contexts) adds it with
+   this one-wave kernel, which -- unlike a framework's multi-wave elementwise kernels -- runs beside a
+   concurrent gather of the other context instead of after it. */
+bre_status bre_film_add(bre_ctx *ctx, int64_t n_floats, float *d_src, float *d_dst, int32_t clear_src);
+/* Pipelined contexts on one device (NULL clears): every later gather of ctx starts its tile kernel only
+   after prev's last tile kernel has finished (an event wait on ctx's stream right before the launch).
+   The segment sort and the other preparation of ctx's gather, and its passes, still run beside prev's
+   gather; only the two tile kernels do not interleave -- their one-wave workgroups would otherwise share
+   the CUs and the L2 two trees at a time (round 6, profiles/r6).  The caller keeps prev alive while
+   ctx gathers. */
+bre_status bre_set_gather_after(bre_ctx *ctx, bre_ctx *prev);
+
 /* ---- multi-GPU gather (SURVEY.md §8(b) `bre_gather_sharded`, §8(e)) ----
    ctxs[0 .. n_ctx): one context per GPU (several contexts on one device are allowed: tests), each
    driven by its own host thread for the duration of the call.  The reference renders in one
@@ -324,6 +339,10 @@ bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, f
      kind 5: the tile kernel's S = aux[0] work roots (k_roots) of the binary tree whose n / 16 Node
              records (bre_device.h: only child[2] and nleaf are read) are x's words; y receives S + 1
              int32 words: the roots largest first (kEmptyChild-padded), then their count
+     kind 6 / 8: the pass chain's stable radix sort (bre_slot.hip) of the n / 2 64-bit (kind 8: n 32-bit)
+             keys in x by bits [aux[0], aux[1]), the values being the input positions; y receives the
+             sorted keys, then the values (int32)
+     kind 7: its exclusive scan of the n int32 words of x; y receives n + 1 int64 (the total last)
    so the tests can hold them against the reference's own primitive tests (src/tests/fp_tests.cpp,
    find_interval.cpp) and against the compiler's correctly rounded sqrt and division. */
 bre_status bre_device_check(bre_ctx *ctx, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
