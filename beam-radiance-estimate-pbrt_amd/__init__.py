@@ -39,7 +39,7 @@ EXPORTS = [
     "bre_camera_pass", "bre_gather_camera", "bre_gather_camera_segments", "bre_get_segments",
     "bre_render_iteration", "bre_render",
     "bre_render_progressive", "bre_shard_segments", "bre_set_beams_sharded", "bre_gather_sharded",
-    "bre_device_check", "bre_resolve_classes", "bre_film_add", "bre_set_gather_after",
+    "bre_device_check", "bre_resolve_classes", "bre_film_add", "bre_set_gather_after", "bre_set_gather_events",
 ]
 
 
@@ -153,6 +153,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.bre_film_add.restype = I32
         lib.bre_set_gather_after.argtypes = [P, P]
         lib.bre_set_gather_after.restype = I32
+        lib.bre_set_gather_events.argtypes = [P, P, P]
+        lib.bre_set_gather_events.restype = I32
     if hasattr(lib, "bre_device_check"):  # (absent from round-3 libraries loaded for A/B timing)
         lib.bre_device_check.argtypes = [P, I32, I64, P, I32, P, P]
         lib.bre_device_check.restype = I32
@@ -276,6 +278,12 @@ class BeamGather:
         contexts on one device; None clears)."""
         self._after = prev  # prev must outlive the gathers that wait for it
         self._check(self.lib.bre_set_gather_after(self.h, prev.h if prev is not None else None))
+
+    def set_gather_events(self, start=None, end=None):
+        """bre_set_gather_events: torch.cuda.Event pair (enable_timing, already recorded once so that the
+        HIP event exists) recorded by libbre around the tile kernel of every later gather; None clears."""
+        h = lambda e: None if e is None else int(e.cuda_event)  # noqa: E731
+        self._check(self.lib.bre_set_gather_events(self.h, h(start), h(end)))
 
     def set_stream(self, stream_handle: int | None):
         self._check(self.lib.bre_set_stream(self.h, stream_handle))

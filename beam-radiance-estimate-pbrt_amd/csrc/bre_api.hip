@@ -142,6 +142,7 @@ struct bre_ctx {
     bre_ctx *after = nullptr;
     hipEvent_t tile_ev = nullptr;  // recorded after each tile-kernel launch (created on first use)
     bool tile_ev_valid = false;
+    hipEvent_t user_ev[2] = {nullptr, nullptr};  // bre_set_gather_events
 };
 
 namespace {
@@ -673,6 +674,8 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         // tile kernel, the last one marks this context's
         ac.wait_ev = (off == 0 && c->after && c->after->tile_ev_valid) ? c->after->tile_ev : nullptr;
         ac.done_ev = off + chunk >= nseg ? c->tile_ev : nullptr;
+        ac.user_start = off == 0 ? c->user_ev[0] : nullptr;
+        ac.user_end = off + chunk >= nseg ? c->user_ev[1] : nullptr;
         ac.nseg = std::min(chunk, nseg - off);
         ac.o = o + 3 * off;
         ac.p = p + 3 * off;
@@ -1456,6 +1459,13 @@ bre_status bre_resolve_classes(bre_ctx *c, int64_t npix, const float *d_classes,
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
     HIPCHK(c, launch_resolve_classes(3 * npix, BRE_FILM_CLASSES, d_classes, d_out, c->stream));
+    return BRE_OK;
+}
+
+bre_status bre_set_gather_events(bre_ctx *c, void *start_event, void *end_event) {
+    if (!c) return BRE_ERR_INVALID_ARG;
+    c->user_ev[0] = static_cast<hipEvent_t>(start_event);
+    c->user_ev[1] = static_cast<hipEvent_t>(end_event);
     return BRE_OK;
 }
 

@@ -196,6 +196,7 @@ struct GatherArgs {
     unsigned int *segbox;  // tile kernel: 6 ordered uints of scratch (the launch's segment box)
     hipEvent_t wait_ev = nullptr;  // tile kernel: the stream waits for it right before the launch (null: no wait)
     hipEvent_t done_ev = nullptr;  // tile kernel: recorded right after the launch (null: none)
+    hipEvent_t user_start = nullptr, user_end = nullptr;  // caller's timing events (bre_set_gather_events)
 };
 
 // capsule-chunk index (bre_chunk.hip)

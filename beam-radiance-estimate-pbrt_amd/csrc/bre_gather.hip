@@ -1662,6 +1662,10 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         const hipError_t ew = hipStreamWaitEvent(s, a.wait_ev, 0);
         if (ew != hipSuccess) return ew;
     }
+    if (a.user_start) {  // the caller's timing: the tile kernel alone (bre_set_gather_events)
+        const hipError_t es = hipEventRecord(a.user_start, s);
+        if (es != hipSuccess) return es;
+    }
 #define BRE_LAUNCH_TILE(C, W)                                                                                    \
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nodes4, a.nvalid,        \
@@ -1687,6 +1691,10 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     if (e4 != hipSuccess) return e4;
     if (a.done_ev) {
         e4 = hipEventRecord(a.done_ev, s);
+        if (e4 != hipSuccess) return e4;
+    }
+    if (a.user_end) {
+        e4 = hipEventRecord(a.user_end, s);
         if (e4 != hipSuccess) return e4;
     }
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + kPassBlock - 1) / kPassBlock)), dim3(kPassBlock), 0, s, a.nseg, a.partial, pcnt,

@@ -253,6 +253,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a_, b_ in events:  # create the HIP events (torch makes them on first record) before libbre records them
+        a_.record()
+        b_.record()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -421,6 +424,8 @@ def config_leg(args, bre, dmod, dev, name, world, rank, iteration=0):
         c, st = make_context(bre, a, dev)
         wl = SceneWorkload(a, bre, [(c, st)], frame, rank, world)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        ev[1].record()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -771,14 +776,14 @@ class SceneWorkload:
                 n = g.camera_pass(self.scene, self.W, self.H, it, a.max_depth, True, True, surface=ld)
             else:
                 n = int(rec["tmax"].shape[0])
-            if ev is not None:
-                ev[0].record()
+            if ev is not None:  # libbre records them around the tile kernel itself (bre_set_gather_events)
+                g.set_gather_events(*ev)
             if rec is None:
                 g.gather_camera(R, ld)  # asynchronous: the next step's passes overlap it on the other stream
             else:  # the C-ABI boundary: caller-order device segments, sorted and gathered inside libbre
                 g.gather_device(rec["o"], rec["p"], rec["d"], rec["tmax"], rec["pixel"], R, self.W * self.H, accum=ld)
             if ev is not None:
-                ev[1].record()
+                g.set_gather_events(None, None)
             if self._last_add is not None:
                 st.wait_event(self._last_add)
             g.film_add(ld, film, clear_src=True)  # film += ld; ld = 0
@@ -886,12 +891,12 @@ class SyntheticWorkload:
         g, dB, dS = self.g, self.dB, self.dS
         acc = self.scratch if scratch else self.frame.accum
         g.set_beams_device(dB["start"], dB["end"], dB["radius"], dB["power"])
-        if ev is not None:
-            ev[0].record()
+        if ev is not None:  # around the tile kernel (bre_set_gather_events)
+            g.set_gather_events(*ev)
         g.gather_device(dS["o"], dS["p"], dS["d"], dS["tmax"], dS["pixel"], self.args.radius, self.frame.npix,
                         accum=acc)
         if ev is not None:
-            ev[1].record()
+            g.set_gather_events(None, None)
         return self.nseg
 
     def diagnostics(self, k=0):

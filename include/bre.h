@@ -234,6 +234,12 @@ bre_status bre_film_add(bre_ctx *ctx, int64_t n_floats, float *d_src, float *d_d
    the CUs and the L2 two trees at a time (round 6, profiles/r6).  The caller keeps prev alive while
    ctx gathers. */
 bre_status bre_set_gather_after(bre_ctx *ctx, bre_ctx *prev);
+/* Timing (NULL, NULL clears): every later gather of the tile kernels (kernels 0 / 4) records the caller's
+   hipEvent_t start_event on the context's stream right before its first tile-kernel launch (after any
+   bre_set_gather_after wait) and end_event right after its last one, so their elapsed time is the tile
+   kernel alone -- not the segment sort before it, the per-segment reduce and film compose after it, or
+   the wait for a pipelined context's gather. */
+bre_status bre_set_gather_events(bre_ctx *ctx, void *start_event, void *end_event);
 
 /* ---- multi-GPU gather (SURVEY.md §8(b) `bre_gather_sharded`, §8(e)) ----
    ctxs[0 .. n_ctx): one context per GPU (several contexts on one device are allowed: tests), each
