@@ -112,6 +112,7 @@ def parse(argv=None):
     ap.add_argument("--gather-fence", type=int, default=1,
                     help="pipelined contexts: 1 = a context's tile kernel waits for the other's last one "
                          "(bre_set_gather_after), 0 = the two gathers may interleave")
+    ap.add_argument("--gather-priority", type=int, default=0, help=argparse.SUPPRESS)  # study: context 0 high priority
     ap.add_argument("--shard-mode", choices=["packets", "tiles", "roots"], default="packets",
                     help="strong scaling: each GPU gathers a range of the sorted segment packets (default) "
                          "or owns image tiles")
@@ -223,10 +224,11 @@ def main():
     frame = dmod.ShardedFrame(args.width, args.height, srank, scount, device=dev, block=args.shard_block,
                               packets=args.shard_mode == "packets", roots=args.shard_mode == "roots",
                               classes=classes)
-    def make_ctx():
-        return make_context(bre, args, dev)
+    def make_ctx(priority=0):
+        return make_context(bre, args, dev, priority)
 
-    g, stream = make_ctx()
+    # --gather-priority 1: the first context's stream at a higher priority than the second's (study)
+    g, stream = make_ctx(-1 if args.gather_priority else 0)
     torch.cuda.set_stream(stream)
 
     if args.workload != "synthetic":
@@ -468,7 +470,7 @@ def config_leg(args, bre, dmod, dev, name, world, rank, iteration=0):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
-def make_context(bre, args, dev):
+def make_context(bre, args, dev, priority=0):
     """One libbre context with the bench's options, on its own torch stream (the HIP events that time
     the gather are recorded on the stream the kernel runs on).  Returns (context, stream)."""
     import torch
@@ -488,7 +490,7 @@ def make_context(bre, args, dev):
             c.set_option(opt, val)
     if film_classes(args) > 1:
         c.set_film_classes(bre.FILM_CLASSES)
-    st = torch.cuda.Stream(dev)
+    st = torch.cuda.Stream(dev, priority=priority)
     c.set_stream(st.cuda_stream)
     return c, st
 
