@@ -67,7 +67,8 @@ struct bre_ctx {
     bool prefilter = true;
     int stack_cap = 0;       // internal: traversal stack entries to use (0 = all; tests force an overflow)
     int block_map = 3;       // internal: tile kernel block mapping (GatherArgs::block_map): 3 LPT (roots by size), 1 rotated
-    int tscan = 4;           // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off
+    int tscan = -1;          // internal: tile kernel transposed-scan threshold (GatherArgs::tscan), 0 = off,
+                             // -1 = by the gather's MaxDistance (tscan_for; 4 fixed until round 6)
                              // (round 5: 4 over 6, C2 +0.5%, C3 +4.8%, profiles/r5/run20, run22)
     int margin = 1;          // internal: tile kernel prefilter margins (GatherArgs::margin)
     int split_records = 0;   // internal: 1 = never carry the power in BeamRec (A/B of the layouts)
@@ -552,6 +553,14 @@ bre_status check_flags(bre_ctx *c) {
     return fail(c, BRE_ERR_INVALID_ARG, "bre_gather: seg_pixel out of [0, npix): segments were skipped");
 }
 
+// The transposed-scan threshold by the gather's MaxDistance (option 108 = -1, the default since round 6).
+// A tile is scanned transposed when its on-lanes * 8 < kept beams * t; the best t falls as the pass rate of
+// the lane tests rises, and that rate grows with MaxDistance against the packets' bundle spread (~0.06-0.12
+// in the unit-box scenes).  Measured on one box (profiles/r6/e6, sums bit-identical for every t): C2
+// iteration 0 (MaxDistance 0.02) 252.8 / 254.2 / 257.3 ms for t = 3 / 4 / 5, iteration 15 (0.005) 110.4 /
+// 108.9 / 108.3 ms; C3 iteration 0 (0.02) 2965 / 3001 / 3064 ms.
+int tscan_for(float maxd) { return maxd >= 0.015f ? 3 : (maxd >= 0.008f ? 4 : 5); }
+
 bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *p, const float *d, const float *tmax,
                          const int32_t *pixel, float R, int64_t npix, float *accum, float *seg_rgb,
                          int32_t *seg_counts, const int32_t *seg_index = nullptr) {
@@ -586,7 +595,7 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
     a.prefilter = c->prefilter;
     a.occupancy = c->occupancy;
     a.block_map = c->block_map;
-    a.tscan = c->tscan;
+    a.tscan = c->tscan >= 0 ? c->tscan : tscan_for(R + c->bset.radius);
     a.margin = c->margin;
     a.stack_cap = c->stack_cap;
     c->stats.n_segments = nseg;
@@ -881,9 +890,9 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 3) return fail(c, BRE_ERR_INVALID_ARG, "block map must be 0..3");
         c->block_map = (int)value;
         return BRE_OK;
-    case 108:  // internal: transposed-scan threshold in eighths, 0 = off (sweeps)
-        if (value < 0 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in 0..64");
-        c->tscan = (int)value;
+    case 108:  // internal: transposed-scan threshold in eighths, 0 = off, -1 = by MaxDistance (default; sweeps)
+        if (value < -1 || value > 64) return fail(c, BRE_ERR_INVALID_ARG, "transposed-scan threshold must be in -1..64");
+        c->tscan = (int)value;  // -1: by MaxDistance (tscan_for)
         return BRE_OK;
     case 112:  // internal: per-lane tile line reject, 1 on (default) / 0 off (A/B); 2 = 1 (round-4 scripts)
         if (value < 0 || value > 2) return fail(c, BRE_ERR_INVALID_ARG, "tile axis mode must be 0, 1 or 2");

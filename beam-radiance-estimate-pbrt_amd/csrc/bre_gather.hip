@@ -70,6 +70,24 @@ __device__ __forceinline__ float4 buf_f4(__amdgpu_buffer_rsrc_t r, unsigned int 
 #ifndef BRE_SCAN_STATS
 #define BRE_SCAN_STATS 0
 #endif
+// BRE_WAVE_TIMES 1 (study builds only, profiles/r6/wave_times.py): every tile-kernel wave stores its
+// start and end times (s_memrealtime, the device's 100 MHz clock) into a device array read back by
+// bre_study_wave_times (exported by such builds only): the kernel's dispatch order and tail.
+#ifndef BRE_WAVE_TIMES
+#define BRE_WAVE_TIMES 0
+#endif
+#if BRE_WAVE_TIMES
+constexpr int kWaveTimes = 1 << 22;
+__device__ unsigned long long g_wave_t[2][kWaveTimes];
+#endif
+__device__ __forceinline__ void wave_time(int which, int lane) {
+#if BRE_WAVE_TIMES
+    if (lane == 0 && blockIdx.x < (unsigned)kWaveTimes) g_wave_t[which][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#else
+    (void)which;
+    (void)lane;
+#endif
+}
 __device__ __forceinline__ unsigned long long phase_clock() {
     return BRE_PHASE_TIMING ? (unsigned long long)__builtin_amdgcn_s_memtime() : 0ull;
 }
@@ -861,6 +879,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     }
     if (sub >= roots[S]) return;  // fewer work roots than S (small trees): whole block exits
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    wave_time(0, lane);
     TileShared &sh = shm[w];
     const int64_t s = grp * kTileBlock + threadIdx.x;
     const int64_t seg0 = grp * kTileBlock + (int64_t)__builtin_amdgcn_readfirstlane(w) * 64;  // lane 0 of this wave
@@ -1179,6 +1198,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
             pcnt[2 * ((int64_t)sub * nseg + s) + 1] = (int32_t)a.w;
         }
     }
+    wave_time(1, lane);
     // the production instantiation's own queue length (contribution counting on): what its exact stage ran
     if (!COUNT && !BRE_SCAN_STATS && !BRE_PHASE_TIMING && count_c && lane == 0 && pf.queued != 0ull)
         atomicAdd(&ctr->queued_pairs, pf.queued);
@@ -1710,3 +1730,18 @@ hipError_t launch_zero_outputs(const GatherArgs &a, hipStream_t s) {
 }
 
 }  // namespace bre
+
+#if BRE_WAVE_TIMES
+// study builds only: the last tile-kernel launch's per-block start and end times (zeros for blocks that
+// exited at once), n blocks into out[0..n) and out[n..2n)
+extern "C" int bre_study_wave_times(int64_t n, unsigned long long *out) {
+    if (n > bre::kWaveTimes) n = bre::kWaveTimes;
+    if (hipDeviceSynchronize() != hipSuccess) return 2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bre::g_wave_t), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    if (hipMemcpyFromSymbol(out + n, HIP_SYMBOL(bre::g_wave_t), (size_t)n * 8, (size_t)bre::kWaveTimes * 8,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return 2;
+    return 0;
+}
+#endif
+
