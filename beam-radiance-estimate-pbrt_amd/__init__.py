@@ -276,7 +276,7 @@ class BeamGather:
     def set_gather_after(self, prev: "BeamGather | None"):
         """bre_set_gather_after: this context's tile kernels start after prev's last one (pipelined
         contexts on one device; None clears)."""
-        self._after = prev  # prev must outlive the gathers that wait for it
+        self._after = prev  # bre_destroy(prev) unlinks; the reference keeps prev from being collected first
         self._check(self.lib.bre_set_gather_after(self.h, prev.h if prev is not None else None))
 
     def set_gather_events(self, start=None, end=None):

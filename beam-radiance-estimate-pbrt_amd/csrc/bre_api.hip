@@ -11,6 +11,7 @@
 #include <cstring>
 #include <string>
 #include <initializer_list>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -141,6 +142,7 @@ struct bre_ctx {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     // bre_set_gather_after: this context's tile kernels wait for `after`'s last one (after->tile_ev)
     bre_ctx *after = nullptr;
+    std::vector<bre_ctx *> followers;  // contexts whose `after` is this one (unlinked in bre_destroy)
     hipEvent_t tile_ev = nullptr;  // recorded after each tile-kernel launch (created on first use)
     bool tile_ev_valid = false;
     hipEvent_t user_ev[2] = {nullptr, nullptr};  // bre_set_gather_events
@@ -738,6 +740,16 @@ hipError_t rocprim_free_total_scan(bre_ctx *c, const CamSlots &cs, int64_t nslot
 
 }  // namespace
 
+// bre_set_gather_after links: guarded, since the two contexts may be driven from two host threads
+static std::mutex &link_mu() {
+    static std::mutex m;
+    return m;
+}
+static void unlink_follower(bre_ctx *lead, bre_ctx *f) {
+    auto &v = lead->followers;
+    v.erase(std::remove(v.begin(), v.end(), f), v.end());
+}
+
 extern "C" {
 
 int bre_abi_version(void) { return BRE_ABI_VERSION; }
@@ -767,6 +779,12 @@ bre_status bre_create(int device, bre_ctx **out) {
 
 void bre_destroy(bre_ctx *c) {
     if (!c) return;
+    {
+        // a pipelined partner must not keep waiting on this context's event once it is gone
+        std::lock_guard<std::mutex> lk(link_mu());
+        for (bre_ctx *f : c->followers) f->after = nullptr;
+        if (c->after) unlink_follower(c->after, c);
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevMem *all[] = {&c->in_start, &c->in_end, &c->in_radius, &c->in_power, &c->box,      &c->cent,
@@ -1482,7 +1500,10 @@ bre_status bre_set_gather_after(bre_ctx *c, bre_ctx *prev) {
     if (!c) return BRE_ERR_INVALID_ARG;
     if (prev == c || (prev && prev->device != c->device))
         return fail(c, BRE_ERR_INVALID_ARG, "bre_set_gather_after: another context of the same device");
+    std::lock_guard<std::mutex> lk(link_mu());
+    if (c->after) unlink_follower(c->after, c);
     c->after = prev;
+    if (prev) prev->followers.push_back(c);
     return BRE_OK;
 }
 

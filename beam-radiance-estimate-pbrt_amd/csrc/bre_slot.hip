@@ -16,6 +16,8 @@
 // (radix_sort_pairs is stable too): every result is bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include "bre_device.h"
 
 namespace bre {
@@ -201,6 +203,7 @@ template <typename K>
 hipError_t sort_impl(void *tmp, K *k0, K *k1, int32_t *v0, int32_t *v1, int64_t n, int begin_bit, int end_bit,
                      hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    if (n > (int64_t)INT32_MAX) return hipErrorInvalidValue;  // the digit offsets are int32
     size_t os, ok_, ov;
     (void)sort_tmp_layout<K>(n, &os, &ok_, &ov);
     char *t = static_cast<char *>(tmp);

@@ -231,8 +231,8 @@ bre_status bre_film_add(bre_ctx *ctx, int64_t n_floats, float *d_src, float *d_d
    after prev's last tile kernel has finished (an event wait on ctx's stream right before the launch).
    The segment sort and the other preparation of ctx's gather, and its passes, still run beside prev's
    gather; only the two tile kernels do not interleave -- their one-wave workgroups would otherwise share
-   the CUs and the L2 two trees at a time (round 6, profiles/r6).  The caller keeps prev alive while
-   ctx gathers. */
+   the CUs and the L2 two trees at a time (round 6, profiles/r6).  bre_destroy(prev) unlinks ctx (its
+   later gathers no longer wait). */
 bre_status bre_set_gather_after(bre_ctx *ctx, bre_ctx *prev);
 /* Timing (NULL, NULL clears): every later gather of the tile kernels (kernels 0 / 4) records the caller's
    hipEvent_t start_event on the context's stream right before its first tile-kernel launch (after any
