@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build the tile-kernel profiling ablations (bre_gather.hip BRE_ABLATE 1..4) as separate libraries
+# Build the tile-kernel profiling ablations (BRE_ABLATE 2..5) as separate libraries; since round 6 they
+# need profiles/r6/negative/ablation_switches_r6.patch applied to bre_gather.hip first
 # and time each on the default C2 bench (results are NOT correct images: timing only).
 # Build (here, CPU):  profiles/ablate.sh build
 # Run (GPU box):      profiles/ablate.sh run OUTDIR [bench args]
