@@ -410,11 +410,12 @@ class BeamGather:
     def device_check(self, kind: int, x, aux=None):
         """bre_device_check: libbre's device copies of NextFloatUp/Down (kinds 0/1), the exact
         stage's square root next to sqrtf (2), FindInterval over aux (3) and the shared-reciprocal
-        division next to x / aux[0] (4).  Returns float32 [n] or [n, 2]."""
+        division next to x / aux[0] (4), the passes' expf / logf / sinf / cosf (9).  Returns float32
+        [n], [n, 2] (kinds 2, 4) or [n, 4] (kind 9)."""
         x = np.ascontiguousarray(x, dtype=np.float32)
         n = x.shape[0]
-        two = kind in (2, 4)
-        y = np.zeros((n, 2) if two else n, np.float32)
+        w = 4 if kind == 9 else 2 if kind in (2, 4) else 1
+        y = np.zeros((n, w) if w > 1 else n, np.float32)
         a = None if aux is None else np.ascontiguousarray(aux, dtype=np.float32)
         self._check(self.lib.bre_device_check(self.h, kind, n, _ptr(x), 0 if a is None else a.shape[0],
                                               None if a is None else _ptr(a), _ptr(y)))

@@ -1927,9 +1927,9 @@ int64_t bre_shard_segments(int64_t n_segments, int32_t rank, int32_t count, int3
 bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,
                             float *y) {
     if (!c) return BRE_ERR_INVALID_ARG;
-    if (kind < 0 || kind > 8) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 8]", kind);
+    if (kind < 0 || kind > 9) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d not in [0, 9]", kind);
     if (n < 0 || (n > 0 && (!x || !y))) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: bad arrays");
-    if (kind >= 6) {
+    if (kind >= 6 && kind <= 8) {
         // the pass chain's one-wave primitives (bre_slot.hip) on caller data
         bre_status st = set_device(c);
         if (st != BRE_OK) return st;
@@ -1991,12 +1991,12 @@ bre_status bre_device_check(bre_ctx *c, int32_t kind, int64_t n, const float *x,
         HIPCHK(c, hipStreamSynchronize(c->stream));
         return BRE_OK;
     }
-    const bool need_aux = kind >= 3;
+    const bool need_aux = kind == 3 || kind == 4;
     if (need_aux && (n_aux < 1 || !aux)) return fail(c, BRE_ERR_INVALID_ARG, "bre_device_check: kind %d needs aux", kind);
     if (n == 0) return BRE_OK;
     bre_status st = set_device(c);
     if (st != BRE_OK) return st;
-    const int64_t outs = (kind == 2 || kind == 4) ? 2 * n : n;
+    const int64_t outs = kind == 9 ? 4 * n : (kind == 2 || kind == 4) ? 2 * n : n;
     HIPCHK(c, c->chk_x.ensure((size_t)n * 4));
     HIPCHK(c, c->chk_y.ensure((size_t)outs * 4));
     HIPCHK(c, c->chk_aux.ensure(need_aux ? (size_t)n_aux * 4 : 4));

@@ -21,7 +21,8 @@ namespace {
 
 // kind 0: next_up; 1: next_down; 2: sqrt_cr_noscale and sqrtf (two outputs per input);
 // 3: find_interval over aux[0, n_aux) with pred aux[i] <= x (the index as a float);
-// 4: div_by_shared(x, aux[0], 1 / aux[0]) and x / aux[0] (two outputs per input)
+// 4: div_by_shared(x, aux[0], 1 / aux[0]) and x / aux[0] (two outputs per input);
+// 9: the passes' expf, logf, sinf and cosf (include/bre_fmath.h; four outputs per input)
 __global__ __launch_bounds__(256) void k_check(int kind, int64_t n, const float *__restrict__ x, int n_aux,
                                                const float *__restrict__ aux, float *__restrict__ y) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -35,6 +36,12 @@ __global__ __launch_bounds__(256) void k_check(int kind, int64_t n, const float 
         y[2 * i + 1] = sqrtf(v);
         break;
     case 3: y[i] = (float)find_interval(n_aux, [&](int k) { return aux[k] <= v; }); break;
+    case 9:
+        y[4 * i] = bre_expf(v);
+        y[4 * i + 1] = bre_logf(v);
+        y[4 * i + 2] = bre_sinf(v);
+        y[4 * i + 3] = bre_cosf(v);
+        break;
     default: {
         const float b = aux[0];
         const float inv = 1.0f / b;
@@ -46,7 +53,7 @@ __global__ __launch_bounds__(256) void k_check(int kind, int64_t n, const float 
 
 }  // namespace
 
-// outputs per input: 1 for kinds 0, 1, 3; 2 for kinds 2 and 4
+// outputs per input: 1 for kinds 0, 1, 3; 2 for kinds 2 and 4; 4 for kind 9
 hipError_t launch_device_check(int kind, int64_t n, const float *x, int n_aux, const float *aux, float *y,
                                hipStream_t s) {
     if (n <= 0) return hipSuccess;

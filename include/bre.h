@@ -349,6 +349,8 @@ bre_status bre_resolve_image(int64_t npix, const float *ld_rgb, int iteration, f
              keys in x by bits [aux[0], aux[1]), the values being the input positions; y receives the
              sorted keys, then the values (int32)
      kind 7: its exclusive scan of the n int32 words of x; y receives n + 1 int64 (the total last)
+     kind 9: y[4i .. 4i + 3] = expf, logf, sinf, cosf of x[i] as the photon and camera passes compute
+             them (include/bre_fmath.h: the x86-64 glibc libm's results bit for bit)
    so the tests can hold them against the reference's own primitive tests (src/tests/fp_tests.cpp,
    find_interval.cpp) and against the compiler's correctly rounded sqrt and division. */
 bre_status bre_device_check(bre_ctx *ctx, int32_t kind, int64_t n, const float *x, int32_t n_aux, const float *aux,

@@ -32,9 +32,12 @@
 //     constructor arguments right to left on x86-64 (checked with this image's g++ on a
 //     stand-alone snippet), so x = second draw, y = first draw.
 //   * Transcendentals (log, exp, sin, cos) come from include/bre_fmath.h on both sides, so the
-//     GPU pass and this restatement agree bit for bit; they are within 2 ulp of libm.  With
-//     ora_set_libm(1) the oracle uses the host libm instead, as the reference does
-//     (tests/test_faithful.py measures what that changes).
+//     GPU pass and this restatement agree bit for bit.  Since round 6 they return the host glibc
+//     libm's expf / logf / sinf / cosf bits for every float input (glibc >= 2.28's algorithms,
+//     x86-64 FMA variants; tests/test_fmath_libm.py): the reference built on this image computes
+//     the same.  (The libm of an older build differs: the Dockerfile pbrt-v3 ships names Ubuntu
+//     12.04, glibc 2.15, whose float routines are other algorithms.)  With ora_set_libm(1) the
+//     oracle calls the host libm itself (tests/test_faithful.py: nothing changes).
 //   * Scene geometry: pbrt Triangles (include/bre_scene.h) -- Triangle::Intersect (watertight,
 //     src/shapes/triangle.cpp:177-300), Triangle::Sample / Area (:535-568), one DiffuseAreaLight per
 //     emitting triangle chosen by power (ComputeLightPowerDistribution, integrator.cpp:217-225;

@@ -29,10 +29,11 @@ static const Float MaxFloat = 3.402823466e+38f;
 static inline Float gamma(int n) { return (n * MachineEpsilon) / (1 - n * MachineEpsilon); }
 
 // Transcendentals.  By default the oracle uses the same restatements as the GPU
-// (include/bre_fmath.h, within 2 ulp of libm) so photon and camera paths agree bit for bit; with
-// ora_set_libm(1) it calls the host libm (std::exp / std::log / std::sin / std::cos) as the
-// reference does (spectrum.h:222-224, homogeneous.cpp:47, grid.cpp:76,104, sampling.cpp:127) --
-// used to measure what that substitution changes in the image (tests/test_faithful.py).
+// (include/bre_fmath.h) so photon and camera paths agree bit for bit; with ora_set_libm(1) it calls
+// the host libm (std::exp / std::log / std::sin / std::cos) as the reference does
+// (spectrum.h:222-224, homogeneous.cpp:47, grid.cpp:76,104, sampling.cpp:127).  Since round 6
+// bre_fmath.h returns libm's bits for every float input (tests/test_fmath_libm.py), so the switch
+// changes nothing (tests/test_faithful.py holds that).
 extern int g_ora_libm;
 static inline Float ora_exp(Float x) { return g_ora_libm ? std::exp(x) : bre_expf(x); }
 static inline Float ora_log(Float x) { return g_ora_libm ? std::log(x) : bre_logf(x); }

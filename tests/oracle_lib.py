@@ -76,8 +76,8 @@ class Oracle:
 
     # -- primitives --
     def set_libm(self, on: bool):
-        """Reference-faithful transcendentals: std::exp / std::log / std::sin / std::cos (the host libm,
-        as pbrt calls them) instead of the Cephes restatement the GPU shares (include/bre_fmath.h)."""
+        """The host libm's std::exp / std::log / std::sin / std::cos (as pbrt calls them) instead of the
+        restatement the GPU shares (include/bre_fmath.h; since round 6 the same bits for every input)."""
         self.lib.ora_set_libm(int(bool(on)))
 
     def slab_pad(self) -> float:

@@ -3,12 +3,14 @@
 Written from the reference text (src/integrators/photonbeam.cpp:258-325, 383-421 and the pbrt
 functions they call), NOT from oracle/bre_oracle_photon.cpp, with every float operation done on
 numpy float32 scalars (IEEE single, like the reference's `Float`) and `Cross` in Python floats
-(double, geometry.h:957-963).  The transcendentals restate include/bre_fmath.h (Cephes) in the
-same float32 arithmetic.  Slow (pure Python): used on a few hundred photons to pin the C++ oracle.
+(double, geometry.h:957-963).  The transcendentals are the host libm's expf / logf / sinf / cosf,
+called through ctypes, as the reference calls them.  Slow (pure Python): used on a few hundred
+photons to pin the C++ oracle.
 """
 from __future__ import annotations
 
 import ctypes
+import ctypes.util
 import math
 import struct
 
@@ -33,110 +35,27 @@ def _from_bits(u):
     return np.array(u & 0xFFFFFFFF, np.uint32).view(np.float32)[()]
 
 
-# ---- include/bre_fmath.h restated ----
-def _roundf(x):
-    big = f32(8388608.0)
-    a = -x if x < 0 else x
-    if not (a < big):
-        return x
-    r = f32(a + f32(0.5))
-    t = f32(f32(r + big) - big)
-    if t > r:
-        t = f32(t - f32(1))
-    return -t if x < 0 else t
-
-
-def _pow2i(n):
-    return _from_bits((n + 127) << 23)
+# ---- transcendentals: the host libm itself, as the reference calls it (std::exp / std::log /
+# std::sin / std::cos on a Float: expf, logf, sinf, cosf; spectrum.h:222-224, homogeneous.cpp:47,74,
+# sampling.cpp:127, medium.cpp:194-213).  include/bre_fmath.h, which the oracle and the GPU use,
+# returns these bits for every float input (tests/fmath_libm_check.c). ----
+_libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+for _name in ("expf", "logf", "sinf", "cosf"):
+    getattr(_libm, _name).argtypes = [ctypes.c_float]
+    getattr(_libm, _name).restype = ctypes.c_float
 
 
 def logf(x):
-    x = f32(x)
-    u = _bits(x)
-    e = (u >> 23) & 0xFF
-    if e == 0:
-        x = f32(x * f32(16777216.0))
-        u = _bits(x)
-        e = ((u >> 23) & 0xFF) - 24
-    e -= 126
-    m = _from_bits((u & 0x807FFFFF) | 0x3F000000)
-    if m < f32(0.70710678118654752440):
-        e -= 1
-        m = f32(f32(m + m) - f32(1))
-    else:
-        m = f32(m - f32(1))
-    z = f32(m * m)
-    y = f32(7.0376836292e-2)
-    for c in (-1.1514610310e-1, 1.1676998740e-1, -1.2420140846e-1, 1.4249322787e-1, -1.6668057665e-1,
-              2.0000714765e-1, -2.4999993993e-1, 3.3333331174e-1):
-        y = f32(f32(y * m) + f32(c))
-    y = f32(f32(y * m) * z)
-    fe = f32(e)
-    y = f32(y + f32(f32(-2.12194440e-4) * fe))
-    y = f32(y + f32(f32(-0.5) * z))
-    r = f32(m + y)
-    return f32(r + f32(f32(0.693359375) * fe))
+    return f32(_libm.logf(float(f32(x))))
 
 
 def expf(x):
-    x = f32(x)
-    if x > f32(88.72283935546875):
-        return INF
-    if x < f32(-103.972084045410):
-        return f32(0)
-    n = _roundf(f32(x * f32(1.44269504088896341)))
-    r = f32(x - f32(n * f32(0.693359375)))
-    r = f32(r - f32(n * f32(-2.12194440e-4)))
-    z = f32(r * r)
-    p = f32(1.9875691500e-4)
-    for c in (1.3981999507e-3, 8.3334519073e-3, 4.1665795894e-2, 1.6666665459e-1, 5.0000001201e-1):
-        p = f32(f32(p * r) + f32(c))
-    p = f32(f32(f32(p * z) + r) + f32(1))
-    ni = int(n)
-    if ni < -126:
-        p = f32(p * _pow2i(-126))
-        ni += 126
-        if ni < -126:
-            return f32(0)
-    if ni > 127:
-        p = f32(p * _pow2i(127))
-        ni -= 127
-    return f32(p * _pow2i(ni))
+    return f32(_libm.expf(float(f32(x))))
 
 
 def sincosf(x):
-    x = f32(x)
-    sign_s = f32(1)
-    if x < 0:
-        x = -x
-        sign_s = f32(-1)
-    j = int(f32(x * f32(1.27323954473516)))
-    if j & 1:
-        j += 1
-    y = f32(j)
-    j &= 7
-    z = f32(f32(f32(x - f32(y * f32(0.78515625))) - f32(y * f32(2.4187564849853515625e-4)))
-            - f32(y * f32(3.77489497744594108e-8)))
-    sign_c = f32(1)
-    if j > 3:
-        j -= 4
-        sign_s = -sign_s
-        sign_c = -sign_c
-    if j > 1:
-        sign_c = -sign_c
-    zz = f32(z * z)
-    ps = f32(-1.9515295891e-4)
-    ps = f32(f32(ps * zz) + f32(8.3321608736e-3))
-    ps = f32(f32(ps * zz) + f32(-1.6666654611e-1))
-    ps = f32(f32(f32(ps * zz) * z) + z)
-    pc = f32(2.443315711809948e-5)
-    pc = f32(f32(pc * zz) + f32(-1.388731625493765e-3))
-    pc = f32(f32(pc * zz) + f32(4.166664568298827e-2))
-    pc = f32(f32(pc * zz) * zz)
-    pc = f32(f32(pc - f32(f32(0.5) * zz)) + f32(1))
-    if j in (1, 2):
-        return f32(sign_s * pc), f32(sign_c * ps)
-    return f32(sign_s * ps), f32(sign_c * pc)
+    x = float(f32(x))
+    return f32(_libm.sinf(x)), f32(_libm.cosf(x))
 
 
 # ---- PCG32 (rng.h) ----

@@ -4,8 +4,8 @@ Pins, in order of strength:
 * PCG32: the published test vector of the PCG reference implementation (pcg32_srandom(42, 54));
 * Henyey-Greenstein: the reference's own tests, src/tests/hg.cpp:10-81, restated (sampling
   consistent with p, orientation for g = +-0.95, normalisation);
-* include/bre_fmath.h against float64 numpy (<= 2 ulp), and bit-for-bit against a float32 Python
-  transliteration (tests/refpy_photon.py);
+* include/bre_fmath.h against float64 numpy (<= 2 ulp), and bit-for-bit against the host libm the
+  reference calls (tests/test_fmath_libm.py: every float input);
 * the whole photon pass against an independent pure-Python restatement (refpy_photon.py) for a
   few hundred photons, bit for bit;
 * size-independent properties of the pass (determinism, 2^maxdepth - 1 bound, vacuum paths).
@@ -79,11 +79,14 @@ def test_fmath_edges(oracle):
     assert 0 < e < 1.2e-38 and abs(float(e) - float(np.float32(np.exp(-100.0)))) <= 1.5e-45  # 1 subnormal ulp
 
 
-def test_fmath_matches_python_transliteration(oracle):
+def test_fmath_matches_libm(oracle):
+    """include/bre_fmath.h (the oracle's and the GPU's transcendentals) against the host libm's expf /
+    logf / sinf / cosf, the functions the reference calls: bit for bit (tests/test_fmath_libm.py runs
+    the C comparison over a sweep of all float bit patterns)."""
     rng = np.random.default_rng(11)
-    xl = rng.uniform(1e-6, 1.0, 300).astype(np.float32)
-    xe = rng.uniform(-30, 5, 300).astype(np.float32)
-    xs = rng.uniform(-3.2, 7.0, 300).astype(np.float32)
+    xl = np.concatenate([rng.uniform(1e-6, 1.0, 3000), 10.0 ** rng.uniform(-44, 38, 1000)]).astype(np.float32)
+    xe = np.concatenate([rng.uniform(-104, 89, 3000), rng.uniform(-30, 5, 1000)]).astype(np.float32)
+    xs = np.concatenate([rng.uniform(-3.2, 7.0, 3000), rng.uniform(-1e4, 1e4, 1000)]).astype(np.float32)
     assert np.array_equal(oracle.fmath("log", xl), np.array([rp.logf(v) for v in xl], np.float32))
     assert np.array_equal(oracle.fmath("exp", xe), np.array([rp.expf(v) for v in xe], np.float32))
     assert np.array_equal(oracle.fmath("sin", xs), np.array([rp.sincosf(v)[0] for v in xs], np.float32))
