@@ -39,8 +39,7 @@ __global__ __launch_bounds__(256) void k_check(int kind, int64_t n, const float 
     case 9:
         y[4 * i] = bre_expf(v);
         y[4 * i + 1] = bre_logf(v);
-        y[4 * i + 2] = bre_sinf(v);
-        y[4 * i + 3] = bre_cosf(v);
+        bre_sincosf(v, &y[4 * i + 2], &y[4 * i + 3]);
         break;
     default: {
         const float b = aux[0];

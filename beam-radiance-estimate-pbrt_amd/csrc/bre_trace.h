@@ -381,7 +381,11 @@ __device__ __forceinline__ float smp_1d(Pcg &r) { return pcg_float(r); }
 // HomogeneousMedium::Tr, homogeneous.cpp:44-48
 __device__ __forceinline__ void medium_tr(const DevScene &S, f3 d, float tmax, float tr[3]) {
     const float x = smin(tmax * len3(d), kMaxFloat);
-    for (int c = 0; c < 3; ++c) tr[c] = bre_expf(-S.sigma_t[c] * x);
+    // one expf per distinct argument (a grey medium's three channels share theirs: the same values)
+    const float a0 = -S.sigma_t[0] * x, a1 = -S.sigma_t[1] * x, a2 = -S.sigma_t[2] * x;
+    tr[0] = bre_expf(a0);
+    tr[1] = a1 == a0 ? tr[0] : bre_expf(a1);
+    tr[2] = a2 == a1 ? tr[1] : bre_expf(a2);
 }
 
 // HomogeneousMedium::Sample distance part, homogeneous.cpp:50-60 (two draws)

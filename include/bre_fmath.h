@@ -235,10 +235,40 @@ BRE_HD float bre_cosf(float y) {
     return bre_sinf_poly(x * s, x * x, (q & 2) ? 1 : 0, n ^ 1);
 }
 
-/* std::sin and std::cos of one argument (g++ may fuse the two calls into sincosf: the same values) */
-BRE_HD void bre_sincosf(float x, float *s, float *c) {
-    *s = bre_sinf(x);
-    *c = bre_cosf(x);
+/* std::sin and std::cos of one argument with one reduction (glibc's sincosf: the same values as
+   sinf and cosf, which take the same reduction, sign and coefficient set; g++ itself fuses the
+   reference's sin / cos pairs into sincosf) */
+BRE_HD void bre_sincosf(float y, float *sinp, float *cosp) {
+    double x = y;
+    const uint32_t at = (bre_f2u(y) >> 20) & 0x7ff;
+    int n;
+    if (at < 0x3f4) {
+        if (at < 0x398) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        *sinp = bre_sinf_poly(x, x2, 0, 0);
+        *cosp = bre_sinf_poly(x, x2, 0, 1);
+        return;
+    }
+    int q;
+    if (at < 0x42f) {
+        x = bre_reduce_fast(x, &n);
+        q = n;
+    } else if (at < 0x7f8) {
+        const uint32_t xi = bre_f2u(y);
+        x = bre_reduce_large(xi, &n);
+        q = n + (int)(xi >> 31);
+    } else {
+        *sinp = *cosp = bre_u2f(0x7fc00000u);
+        return;
+    }
+    const double s = ((q & 3) == 1 || (q & 3) == 2) ? -1.0 : 1.0;
+    const int t = (q & 2) ? 1 : 0;
+    *sinp = bre_sinf_poly(x * s, x * x, t, n);
+    *cosp = bre_sinf_poly(x * s, x * x, t, n ^ 1);
 }
 
 #endif /* BRE_FMATH_H */

@@ -3,9 +3,10 @@
  *
  * The reference calls std::exp / std::log / std::sin / std::cos on floats, i.e. libm's expf, logf,
  * sinf and cosf (spectrum.h:222-224, homogeneous.cpp:47,74, grid.cpp:76,104, sampling.cpp:127,
- * geometry.h SphericalDirection via medium.cpp:194-213).  This program evaluates bre_expf, bre_logf,
- * bre_sinf and bre_cosf and the libm functions on every STRIDE-th float bit pattern (stride 1: all
- * 2^32) in THREADS threads and counts the results that differ in any bit (two NaNs count as equal).
+ * geometry.h SphericalDirection via medium.cpp:194-213).  This program evaluates bre_expf, bre_logf
+ * and bre_sincosf (and that the pair equals bre_sinf / bre_cosf) and the libm functions on every
+ * STRIDE-th float bit pattern (stride 1: all 2^32) in THREADS threads and counts the results that
+ * differ in any bit (two NaNs count as equal).
  *
  *   fmath_libm_check STRIDE THREADS    -> one line per function, exit status 1 if any differ
  *
@@ -30,10 +31,14 @@ static void *run(void *arg) {
     Job *j = (Job *)arg;
     for (uint64_t u = j->begin; u < j->end; u += j->stride) {
         const float x = bre_u2f((uint32_t)u);
-        const float mine[4] = {bre_expf(x), bre_logf(x), bre_sinf(x), bre_cosf(x)};
+        float s, c;
+        bre_sincosf(x, &s, &c);
+        const float mine[4] = {bre_expf(x), bre_logf(x), s, c};
         const float ref[4] = {expf(x), logf(x), sinf(x), cosf(x)};
         for (int k = 0; k < 4; ++k)
             if (!same(mine[k], ref[k]) && j->bad[k]++ == 0) j->first_bad[k] = (uint32_t)u;
+        /* the one-reduction pair equals the two functions (the photon pass calls the pair) */
+        if ((!same(s, bre_sinf(x)) || !same(c, bre_cosf(x))) && j->bad[2]++ == 0) j->first_bad[2] = (uint32_t)u;
         ++j->tested;
     }
     return NULL;
