@@ -88,8 +88,6 @@ struct bre_ctx {
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     unsigned int *rb_host = nullptr;     // pinned words of read_small (kernel readback)
     int kernel_readback = BRE_KERNEL_READBACK;  // internal (option 118): read_small through k_readback
-    int sparse_partials = 1;  // internal (option 120): the tile kernel writes and k_reduce reads only the
-                              // partials of (packet, work root) waves with a contribution (0: all, A/B)
     int slot_passes = 1;  // internal (option 119): the pass chain's scans, sorts and fills by the one-wave
                           // primitives (bre_slot.hip, default) / 0 rocPRIM and hipMemsetAsync (A/B)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -113,7 +111,7 @@ struct bre_ctx {
     // gather staging (host-pointer API)
     DevMem g_o, g_p, g_d, g_tmax, g_pix, g_accum, g_seg_rgb, g_counts;
     DevMem chk_x, chk_aux, chk_y;  // bre_device_check staging
-    DevMem counters_buf, roots, roots_sh, roots_tmp, partial, pcnt, pmask, segrec, tileax, segbox, nodes4;
+    DevMem counters_buf, roots, roots_sh, roots_tmp, partial, pcnt, segrec, tileax, segbox, nodes4;
     // photon pass
     DevMem ph_scene, ph_counts, ph_offsets, ph_tmp, grid_dens;
     DevMem ph_s_start, ph_s_end, ph_s_radius, ph_s_power;  // single-trace photon pass: per-photon beam slots
@@ -672,10 +670,6 @@ bre_status gather_device(bre_ctx *c, int64_t nseg, const float *o, const float *
         HIPCHK(c, c->pcnt.ensure(sizeof(int32_t) * 2 * (size_t)chunk * (size_t)S_eff));
         a.pcnt = c->pcnt.as<int32_t>();
     }
-    if (c->sparse_partials) {
-        HIPCHK(c, c->pmask.ensure(sizeof(unsigned long long) * (size_t)((chunk + 63) / 64) * (size_t)((S_eff + 63) / 64)));
-        a.pmask = c->pmask.as<unsigned long long>();
-    }
     if (c->tile_axis && a.leaf_size > 0) {
         const int64_t ntiles = (c->nvalid + a.leaf_size - 1) / a.leaf_size;
         HIPCHK(c, c->tileax.ensure(sizeof(TileAxis) * (size_t)ntiles));
@@ -797,7 +791,7 @@ void bre_destroy(bre_ctx *c) {
                      &c->cbounds,  &c->nvalid_buf, &c->keys,  &c->keys_alt, &c->vals,     &c->vals_alt,
                      &c->sort_tmp, &c->leaf_parent, &c->visit, &c->recs,    &c->pow,      &c->nodes,
                      &c->g_o,      &c->g_p,    &c->g_d,       &c->g_tmax,   &c->g_pix,    &c->g_accum,
-                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->pmask, &c->segrec,
+                     &c->g_seg_rgb, &c->g_counts, &c->counters_buf, &c->roots, &c->partial, &c->pcnt, &c->segrec,
                      &c->tileax, &c->segbox, &c->nodes4, &c->roots_sh, &c->roots_tmp,
                      &c->ph_scene, &c->ph_counts, &c->ph_offsets, &c->ph_tmp, &c->ph_s_start, &c->ph_s_end, &c->ph_s_radius, &c->ph_s_power, &c->grid_dens, &c->cam_dev, &c->cam_perms,
                      &c->cs_o, &c->cs_p, &c->cs_d, &c->cs_t, &c->cs_pix, &c->cs_valid, &c->cam_offs,
@@ -943,10 +937,6 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
     case 118:  // internal: small device-to-host reads by a one-wave kernel into pinned memory (1) / hipMemcpyAsync (0)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "readback mode must be 0 or 1");
         c->kernel_readback = (int)value;
-        return BRE_OK;
-    case 120:  // internal: sparse tile-kernel partials (1, default) / every (packet, work root) partial (0)
-        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "sparse partials mode must be 0 or 1");
-        c->sparse_partials = (int)value;
         return BRE_OK;
     case 119:  // internal: pass-chain scans / sorts / fills, 1 one-wave primitives (default) / 0 rocPRIM (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "pass primitives mode must be 0 or 1");

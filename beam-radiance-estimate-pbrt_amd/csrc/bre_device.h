@@ -185,9 +185,6 @@ struct GatherArgs {
     int split;             // S, power of two <= kMaxSplit
     float *partial;        // [split][nseg][3]
     int32_t *pcnt;         // [split][nseg][2] per-subtree counts (counters / contribution counting)
-    // [packets][ceil(split / 64)] bit j: the packet's wave on work root j had a contribution, the only
-    // partials written and read (sparse partials, internal option 120); null: every partial (dense)
-    unsigned long long *pmask = nullptr;
     SegRec *segrec;        // [nseg] tile kernel: per-segment records (written by k_seg_prep)
     bool prefilter;
     int occupancy;         // tile kernel register budget: min waves per SIMD (1, 6, 7 or 8)

@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
     int32_t *__restrict__ pcnt, const BeamRec *__restrict__ recs, const float4 *__restrict__ pw, BeamSet bset,
     const Node *__restrict__ nodes, const Node4 *__restrict__ nodes4, int64_t nvalid, int leaf_size,
     const int32_t *__restrict__ roots, int S, DevCounters *ctr, int stack_cap, int prefilter, int map, int tscan,
-    int margin, const TileAxis *__restrict__ tax, unsigned long long *__restrict__ pmask) {
+    int margin, const TileAxis *__restrict__ tax) {
     __shared__ TileShared shm[kTileBlock / 64];
     // Block -> (subtree, packet group).  map 1: block b works on packet group b / S and subtree
     // (b + b / S) mod S, so under the round-robin dispatch over the 8 XCDs every XCD sees every
@@ -1187,17 +1187,9 @@ __global__ __launch_bounds__(kTileBlock, MINW) void k_gather_tile(
         t1 = 0;
     }
     __builtin_amdgcn_wave_barrier();
-    const float4 a = sh.acc[lane];
-    bool store = valid;
-    if (pmask != nullptr) {
-        // sparse partials: a wave with no contribution writes nothing (its partials are +0: k_reduce
-        // skips them, the same sums); the others mark their work root in the packet's mask
-        const bool any = __ballot(valid && a.w != 0.f) != 0ull;
-        store = store && any;
-        if (any && lane == 0) atomicOr(&pmask[grp * ((S + 63) >> 6) + (sub >> 6)], 1ull << (sub & 63));
-    }
-    if (store) {
+    if (valid) {
         float *dst = partial + 3 * ((int64_t)sub * nseg + s);
+        const float4 a = sh.acc[lane];
         dst[0] = a.x;
         dst[1] = a.y;
         dst[2] = a.z;
@@ -1270,30 +1262,13 @@ __global__ __launch_bounds__(kPassBlock) void k_reduce(int64_t nseg, const float
                                                 int S, const int32_t *__restrict__ pixel, int64_t npix,
                                                 float *__restrict__ accum, float *__restrict__ seg_rgb,
                                                 int32_t *__restrict__ seg_counts, const int32_t *__restrict__ seg_index,
-                                                DevCounters *ctr, const unsigned long long *__restrict__ pmask) {
+                                                DevCounters *ctr) {
     const int64_t s = (int64_t)blockIdx.x * kPassBlock + threadIdx.x;
     const bool in = s < nseg;
     const int nr = roots[S];
     float cr = 0.f, cg = 0.f, cb = 0.f;
     long long c = 0, k = 0;
-    if (in && pmask != nullptr) {
-        // sparse partials: only the work roots the packet's mask names, in root order (a skipped
-        // partial is +0 and the sums are >= 0: the dense loop's bits); block = packet (kPassBlock 64)
-        const int W = (S + 63) >> 6;
-        for (int w = 0; w < W; ++w) {
-            unsigned long long m = pmask[(int64_t)blockIdx.x * W + w];
-            while (m != 0ull) {
-                const int j = w * 64 + __ffsll((long long)m) - 1;
-                m &= m - 1ull;
-                const float *q = partial + 3 * ((int64_t)j * nseg + s);
-                cr += q[0];
-                cg += q[1];
-                cb += q[2];
-                if (pcnt) k += pcnt[2 * ((int64_t)j * nseg + s) + 1];
-            }
-        }
-        c = (pcnt && nr > 0) ? -1 : 0;  // the production kernel counts no candidates (-1 per subtree)
-    } else if (in) {
+    if (in) {
         for (int j = 0; j < nr; ++j) {
             const float *q = partial + 3 * ((int64_t)j * nseg + s);
             cr += q[0];
@@ -1304,8 +1279,6 @@ __global__ __launch_bounds__(kPassBlock) void k_reduce(int64_t nseg, const float
                 k += pcnt[2 * ((int64_t)j * nseg + s) + 1];
             }
         }
-    }
-    if (in) {
         const int64_t so = seg_index ? (int64_t)seg_index[s] : s;
         if (seg_rgb) {
             seg_rgb[3 * so] = cr;
@@ -1701,14 +1674,6 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         tax = a.tileax;
     }
     const dim3 grid4((unsigned int)(((a.nseg + kTileBlock - 1) / kTileBlock) * a.split));
-    // sparse partials (production kernel only; the counter instantiation counts every subtree's
-    // candidates): the packets' masks start empty
-    static_assert(kPassBlock == kTileBlock && kTileBlock == 64, "k_reduce reads one packet's mask per block");
-    const unsigned long long *pmask = counters ? nullptr : a.pmask;
-    if (pmask) {
-        const hipError_t ef = slot_fill(a.pmask, ((a.nseg + 63) / 64) * ((a.split + 63) / 64) * 2, 0u, s);
-        if (ef != hipSuccess) return ef;
-    }
     // block map 0 deals S / 8 roots to each XCD: a split that is not a multiple of 8 (work-root shards:
     // ceil(S / count)) would leave roots unassigned, so such launches take the LPT map
     GatherArgs am = a;
@@ -1725,8 +1690,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
     hipLaunchKernelGGL((k_gather_tile<C, W>), grid4, dim3(kTileBlock), 0, s, a.nseg, a.o, a.p, a.d, a.tmax,      \
                        a.segrec, a.R, a.partial, pcnt, a.recs, a.pow, a.bset, a.nodes, a.nodes4, a.nvalid,        \
                        a.leaf_size,                                                                        \
-                       a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, am.block_map, a.tscan, a.margin, tax,  \
-                       C ? nullptr : a.pmask)
+                       a.roots, a.split, a.ctr, stack_cap, (int)a.prefilter, am.block_map, a.tscan, a.margin, tax)
     if (counters) {
         BRE_LAUNCH_TILE(true, 1);
     } else if (a.occupancy == 1) {
@@ -1754,7 +1718,7 @@ hipError_t launch_gather(const GatherArgs &a, int kernel, bool counters, hipStre
         if (e4 != hipSuccess) return e4;
     }
     hipLaunchKernelGGL(k_reduce, dim3((unsigned int)((a.nseg + kPassBlock - 1) / kPassBlock)), dim3(kPassBlock), 0, s, a.nseg, a.partial, pcnt,
-                       a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb, a.seg_counts, a.seg_index, a.ctr, pmask);
+                       a.roots, a.split, a.pixel, a.npix, a.accum, a.seg_rgb, a.seg_counts, a.seg_index, a.ctr);
     return hipGetLastError();
 }
 

@@ -536,44 +536,3 @@ def test_tree_and_segment_orders_give_exact_sets(bre, synth, oracle, beam_key):
         for opt, bad in ((110, 3), (110, -1), (105, 5)):
             with pytest.raises(bre.BreError):
                 g.set_option(opt, bad)
-
-
-@pytest.mark.parametrize("kind", ["camera", "bounce", "long"])
-@pytest.mark.parametrize("split", [1, 64, 256, 1024])
-def test_sparse_partials_are_bit_identical(bre, synth, kind, split):
-    """Sparse partials (internal option 120, the default since round 6): a (packet, work root) wave with
-    no contribution writes no partial, and k_reduce adds only the partials the packet's mask names, in
-    root order.  A skipped partial is +0 and every sum is >= 0, so per-segment RGB, contribution counts,
-    the film and the production candidate marker (-1) are the dense reduce's bits -- also over several
-    launches (a 1 MiB partial cap) and for splits below, at and above one mask word."""
-    if kind == "long":
-        beams = synth.fog_beams(6000, seed=81, radius=0.05, mean_length=0.8)
-        segs = synth.bounce_segments(6000, seed=82)
-        R = 0.08
-    else:
-        beams = synth.fog_beams(20000, seed=83)
-        segs = synth.camera_segments(64, 64, seed=84) if kind == "camera" else synth.bounce_segments(4096, seed=85)
-        R = 0.01
-    n = segs["tmax"].shape[0]
-    npix = 4096
-    pixel = (np.arange(n) * 7 % npix).astype(np.int32)
-    outs = {}
-    for sparse, cap in ((0, -1), (1, -1), (1, 1)):
-        with bre.BeamGather(0, counters=False, kernel=0) as g:
-            g.set_option(bre.OPT_SPLIT, split)
-            g.set_option(120, sparse)
-            if cap > 0:
-                g.set_option(109, cap)
-            g.set_beams(beams["start"], beams["end"], beams["radius"], beams["power"])
-            acc = np.zeros((npix, 3), np.float32)
-            r = g.gather(segs["o"], segs["p"], segs["d"], segs["tmax"], pixel=pixel, R=R, npix=npix, accum=acc,
-                         counts=True)
-            outs[(sparse, cap)] = (r["seg_rgb"], r["counts"], acc)
-    base = outs[(0, -1)]
-    assert base[1][:, 1].sum() > 0 and (base[1][:, 0] == -1).all()
-    for key in ((1, -1), (1, 1)):
-        rgb, cnt, acc = outs[key]
-        assert np.array_equal(rgb.view(np.uint32), base[0].view(np.uint32)), key
-        assert np.array_equal(cnt, base[1]), key
-        # the film: one float atomic per segment per channel, in arrival order -- equal to rounding
-        assert np.allclose(acc, base[2], rtol=1e-6, atol=0), key
