@@ -88,6 +88,8 @@ struct bre_ctx {
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     unsigned int *rb_host = nullptr;     // pinned words of read_small (kernel readback)
     int kernel_readback = BRE_KERNEL_READBACK;  // internal (option 118): read_small through k_readback
+    int coarse_keys = 1;  // internal (option 121): the tree-order and segment sorts on the keys' top 48 bits
+                          // (6 radix passes instead of 8 each; round 6, profiles/r6/e13) / all bits (0)
     int slot_passes = 1;  // internal (option 119): the pass chain's scans, sorts and fills by the one-wave
                           // primitives (bre_slot.hip, default) / 0 rocPRIM and hipMemsetAsync (A/B)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -349,7 +351,7 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
         HIPCHK(c, c->gbox.ensure(N * 6 * sizeof(float)));
         b.gbox = c->gbox.as<float>();
         HIPCHK(c, launch_tree_key(b, nvalid, c->stream));
-        HIPCHK(c, launch_sort(b, c->stream));
+        HIPCHK(c, launch_sort(b, c->stream, 64, c->coarse_keys ? 16 : 0));
     } else {
         b.beam_key = 0;
     }
@@ -938,6 +940,11 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "readback mode must be 0 or 1");
         c->kernel_readback = (int)value;
         return BRE_OK;
+    case 121:  // internal: coarse sort keys (1, default: the tree-order sort on bits [16, 64), the segment
+               // sort on [12, 60): 6 radix passes each instead of 8) / all bits (0)
+        if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "coarse keys mode must be 0 or 1");
+        c->coarse_keys = (int)value;
+        return BRE_OK;
     case 119:  // internal: pass-chain scans / sorts / fills, 1 one-wave primitives (default) / 0 rocPRIM (A/B)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "pass primitives mode must be 0 or 1");
         c->slot_passes = (int)value;
@@ -1403,7 +1410,7 @@ static bre_status gather_segments_core(bre_ctx *c, int64_t n, const float *o, co
     SegSort ss{n, o, p, d, t, pix, c->ss_bounds.as<unsigned int>(), c->ss_keys.as<unsigned long long>(),
                c->ss_keys_alt.as<unsigned long long>(), c->ss_vals.as<int32_t>(), c->ss_vals_alt.as<int32_t>(),
                c->ss_tmp.ptr, tb, c->ss_o.as<float>(), c->ss_p.as<float>(), c->ss_d.as<float>(),
-               c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key, c->slot_passes};
+               c->ss_t.as<float>(), c->ss_pix.as<int32_t>(), c->sort_key, c->slot_passes, c->coarse_keys ? 12 : 0};
     HIPCHK(c, launch_sort_segments(ss, c->stream));
     // ss_vals_alt[i] = the caller's index of sorted segment i (the sort's permutation)
     if (pshard) return pick(ss.o2, ss.p2, ss.d2, ss.t2, ss.pix2, c->ss_vals_alt.as<int32_t>());

@@ -554,13 +554,14 @@ size_t sort_temp_bytes(int64_t n) {
     return std::max(bytes, slot_sort_temp_bytes(n, 8));
 }
 
-hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit) {
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit, int begin_bit) {
     if (b.n == 0) return hipSuccess;
     size_t bytes = b.sort_tmp_bytes;
-    // Morton keys use bits [0, 63), the centroid hash bits [0, 32); invalid beams sort last either way.
-    if (b.slot) return slot_sort_pairs(b.sort_tmp, b.keys, b.keys_alt, b.vals, b.vals_alt, b.n, 0, end_bit, s);
-    return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n, 0,
-                                     (unsigned int)end_bit, s);
+    // Morton keys use bits [0, 63), the centroid hash bits [0, 32); invalid beams (~0) sort last either
+    // way, also from a begin_bit > 0 (bits 60-63 are set only in theirs)
+    if (b.slot) return slot_sort_pairs(b.sort_tmp, b.keys, b.keys_alt, b.vals, b.vals_alt, b.n, begin_bit, end_bit, s);
+    return rocprim::radix_sort_pairs(b.sort_tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (size_t)b.n,
+                                     (unsigned int)begin_bit, (unsigned int)end_bit, s);
 }
 
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s) {

@@ -94,6 +94,7 @@ struct BuildBuffers {
     unsigned int *nvalid;   // 3: valid beams, then the ordered min and max of their radii
     int uniform_radius = 0; // k_pack: the set's BeamSet::uniform (read back after k_prep)
     int slot = 1;           // sorts and fills by the one-wave primitives (bre_slot.hip), 0: rocPRIM / hipMemset
+    int key_lo = 0;         // the tree-order sort skips the key's bits below key_lo (internal option 121)
     unsigned long long *keys, *keys_alt;
     int32_t *vals, *vals_alt;
     void *sort_tmp;
@@ -127,7 +128,7 @@ hipError_t launch_morton(const BuildBuffers &b, hipStream_t s);
 size_t sort_temp_bytes(int64_t n);
 // tree keys 1 / 2: a hash of the centroid for the equal-centroid groups (sorted over 32 bits)
 hipError_t launch_cent_hash(const BuildBuffers &b, hipStream_t s);
-hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit = 64);
+hipError_t launch_sort(const BuildBuffers &b, hipStream_t s, int end_bit = 64, int begin_bit = 0);
 hipError_t launch_pack(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
 // tree key 1, after the centroid sort: group boxes (k_group), then the (start, end) keys into keys/vals
 hipError_t launch_tree_key(const BuildBuffers &b, int64_t nvalid, hipStream_t s);
@@ -262,6 +263,7 @@ struct SegSort {
                    // 2 / 3: the segment's line (dominant-axis class + slopes + plane crossing [+ midpoint]);
                    // 4: Hilbert order of (origin, end point) (the default, bre_math.h hilbert_key)
     int slot = 1;  // the sort by the one-wave radix sort (bre_slot.hip), 0: rocPRIM
+    int key_lo = 0;  // the sort skips the key's bits below key_lo (coarse keys, internal option 121)
 };
 size_t seg_sort_temp_bytes(int64_t n);
 // deterministic per-pixel accumulation of per-segment sums (bre_sort.hip): stable sort of the

@@ -433,8 +433,10 @@ hipError_t launch_sort_segments(const SegSort &s, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.tmp_bytes;
-    e = s.slot ? slot_sort_pairs(s.tmp, s.keys, s.keys_alt, s.vals, s.vals_alt, s.n, 0, key_bits, st)
-               : rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n, 0, key_bits, st);
+    const int lo = s.key_lo < key_bits ? s.key_lo : 0;
+    e = s.slot ? slot_sort_pairs(s.tmp, s.keys, s.keys_alt, s.vals, s.vals_alt, s.n, lo, key_bits, st)
+               : rocprim::radix_sort_pairs(s.tmp, bytes, s.keys, s.keys_alt, s.vals, s.vals_alt, (size_t)s.n,
+                                           (unsigned int)lo, (unsigned int)key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_permute, dim3(grid_of(s.n)), dim3(kBlock), 0, st, s.n, s.vals_alt, s.o, s.p, s.d, s.t,
                        s.pix, s.o2, s.p2, s.d2, s.t2, s.pix2);

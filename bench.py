@@ -102,6 +102,7 @@ def parse(argv=None):
     ap.add_argument("--partial-mib", type=int, default=-1, help=argparse.SUPPRESS)  # option 109: launches per gather
     ap.add_argument("--readback", type=int, default=-1, help=argparse.SUPPRESS)  # option 118 A/B
     ap.add_argument("--slot-passes", type=int, default=-1, help=argparse.SUPPRESS)  # option 119 A/B
+    ap.add_argument("--coarse-keys", type=int, default=-1, help=argparse.SUPPRESS)  # option 121 A/B
     ap.add_argument("--film-classes", type=int, default=1,
                     help="packet shards: keep the film as 8 packet-class planes, gathered and resolved in class "
                          "order, so every N dividing 8 renders the one-GPU film bit for bit (0: one film, "
@@ -485,7 +486,8 @@ def make_context(bre, args, dev, priority=0):
                      (107, args.block_map), (105, args.sort_key), (108, args.tscan), (110, args.beam_key),
                      (111, args.margin), (112, args.tile_axis), (113, args.split_records), (114, args.film_compose),
                      (116, args.photon_single), (117, args.pass_priority),
-                     (109, args.partial_mib), (118, args.readback), (119, args.slot_passes)):
+                     (109, args.partial_mib), (118, args.readback), (119, args.slot_passes),
+                     (121, args.coarse_keys)):
         if val >= 0:
             c.set_option(opt, val)
     if film_classes(args) > 1:

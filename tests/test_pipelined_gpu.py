@@ -129,3 +129,29 @@ def test_gather_events_bracket_the_tile_kernel(bre, scene_mod_gpu):
         g.set_gather_events(None, None)
     tile, whole = t0.elapsed_time(t1), w0.elapsed_time(w1)
     assert 0.0 < tile <= whole
+
+
+def test_coarse_sort_keys_keep_every_pair(bre, scene_mod_gpu):
+    """Internal option 121 (default 1): the tree-order and segment sorts use the keys' top 48 bits.  Only
+    orders change (the tree's leaf tiles, the packets), so every segment keeps its contribution count and
+    its sum to float summation order, in camera-pass order."""
+    import torch
+
+    scene = scene_mod_gpu.cornell_scene(0.05, 0.5, 0.0)
+    R = bre.beam_radius_at(0.01, 0.5, 2)
+    outs = {}
+    for coarse in (0, 1):
+        with bre.BeamGather(0) as g:
+            g.set_option(121, coarse)
+            g.trace_photons(scene, 100_000, 2, 5, R)
+            n = g.camera_pass(scene, 128, 128, 2, 5, True, True)
+            rgb = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+            cnt = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
+            g.gather_camera_segments(R, seg_rgb=rgb, counts=cnt)
+            g.synchronize()
+            outs[coarse] = (rgb.cpu().numpy(), cnt.cpu().numpy())
+    assert outs[0][1][:, 1].sum() > 0
+    assert np.array_equal(outs[0][1][:, 1], outs[1][1][:, 1])
+    c = outs[0][1][:, 1].astype(np.float64)
+    tol = np.maximum(1e-5, 4 * 2.0 ** -24 * np.sqrt(np.maximum(c, 1)))[:, None]
+    assert (np.abs(outs[1][0] - outs[0][0]) <= tol * np.maximum(np.abs(outs[0][0]), 1e-30)).all()
