@@ -351,7 +351,8 @@ bre_status build(bre_ctx *c, int64_t n, const float *start, const float *end, co
         HIPCHK(c, c->gbox.ensure(N * 6 * sizeof(float)));
         b.gbox = c->gbox.as<float>();
         HIPCHK(c, launch_tree_key(b, nvalid, c->stream));
-        HIPCHK(c, launch_sort(b, c->stream, 64, c->coarse_keys ? 16 : 0));
+        b.key_lo = c->coarse_keys ? 16 : 0;  // the hierarchy compares the bits the sort ordered
+        HIPCHK(c, launch_sort(b, c->stream, 64, b.key_lo));
     } else {
         b.beam_key = 0;
     }

@@ -383,30 +383,35 @@ __global__ __launch_bounds__(kBlock) void k_pack(const float *__restrict__ start
     pw[s] = p;
 }
 
-__device__ __forceinline__ int ldelta(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf, int i, int j) {
+// keys are compared from bit key_lo up: the bits the sort ordered (coarse keys, option 121), so the
+// leaves' keys are monotone -- unsorted low bits would give the Karras split a non-monotone sequence
+// and an invalid hierarchy
+__device__ __forceinline__ int ldelta(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf, int i, int j,
+                                      int key_lo) {
     if (j < 0 || j >= nleaf) return -1;
-    const unsigned long long ki = keys[(int64_t)i * leaf_size], kj = keys[(int64_t)j * leaf_size];
+    const unsigned long long ki = keys[(int64_t)i * leaf_size] >> key_lo, kj = keys[(int64_t)j * leaf_size] >> key_lo;
     if (ki == kj) return 64 + __clz((unsigned int)(i ^ j));
     return __clzll(ki ^ kj);
 }
 
 __global__ __launch_bounds__(kBlock) void k_karras(const unsigned long long *__restrict__ keys, int leaf_size, int nleaf,
-                                                   Node *__restrict__ nodes, int32_t *__restrict__ leaf_parent) {
+                                                   Node *__restrict__ nodes, int32_t *__restrict__ leaf_parent,
+                                                   int key_lo) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= nleaf - 1) return;
-    const int d = (ldelta(keys, leaf_size, nleaf, i, i + 1) - ldelta(keys, leaf_size, nleaf, i, i - 1)) >= 0 ? 1 : -1;
-    const int dmin = ldelta(keys, leaf_size, nleaf, i, i - d);
+    const int d = (ldelta(keys, leaf_size, nleaf, i, i + 1, key_lo) - ldelta(keys, leaf_size, nleaf, i, i - 1, key_lo)) >= 0 ? 1 : -1;
+    const int dmin = ldelta(keys, leaf_size, nleaf, i, i - d, key_lo);
     int lmax = 2;
-    while (ldelta(keys, leaf_size, nleaf, i, i + lmax * d) > dmin) lmax <<= 1;
+    while (ldelta(keys, leaf_size, nleaf, i, i + lmax * d, key_lo) > dmin) lmax <<= 1;
     int l = 0;
     for (int t = lmax >> 1; t >= 1; t >>= 1)
-        if (ldelta(keys, leaf_size, nleaf, i, i + (l + t) * d) > dmin) l += t;
+        if (ldelta(keys, leaf_size, nleaf, i, i + (l + t) * d, key_lo) > dmin) l += t;
     const int j = i + l * d;
-    const int dnode = ldelta(keys, leaf_size, nleaf, i, j);
+    const int dnode = ldelta(keys, leaf_size, nleaf, i, j, key_lo);
     int s = 0, t = l;
     do {
         t = (t + 1) >> 1;
-        if (ldelta(keys, leaf_size, nleaf, i, i + (s + t) * d) > dnode) s += t;
+        if (ldelta(keys, leaf_size, nleaf, i, i + (s + t) * d, key_lo) > dnode) s += t;
     } while (t > 1);
     const int gamma = i + s * d + min(d, 0);
     const int lo = min(i, j), hi = max(i, j);
@@ -591,7 +596,7 @@ hipError_t launch_hierarchy(const BuildBuffers &b, int64_t nvalid, hipStream_t s
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_karras, dim3(grid_for(nleaf - 1)), dim3(kBlock), 0, s, b.keys_alt, K, nleaf, b.nodes,
-                       b.leaf_parent);
+                       b.leaf_parent, b.key_lo);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = b.slot ? slot_fill(b.visit, nleaf - 1, 0u, s) : hipMemsetAsync(b.visit, 0, sizeof(unsigned int) * (size_t)(nleaf - 1), s);
