@@ -88,8 +88,10 @@ struct bre_ctx {
     unsigned int *flags_host = nullptr;  // pinned copy of DevCounters::flags (check_flags)
     unsigned int *rb_host = nullptr;     // pinned words of read_small (kernel readback)
     int kernel_readback = BRE_KERNEL_READBACK;  // internal (option 118): read_small through k_readback
-    int coarse_keys = 1;  // internal (option 121): the tree-order and segment sorts on the keys' top 48 bits
-                          // (6 radix passes instead of 8 each; round 6, profiles/r6/e13) / all bits (0)
+    int coarse_keys = 0;  // internal (option 121): 1 = the tree-order and segment sorts on the keys' top 48
+                          // bits (6 radix passes instead of 8 each; round 6, profiles/r6/e13); 0 (default)
+                          // all bits.  Off: its first form hung the full C5 render (the hierarchy saw
+                          // unsorted low bits) and the fixed form is not yet measured on the GPU.
     int slot_passes = 1;  // internal (option 119): the pass chain's scans, sorts and fills by the one-wave
                           // primitives (bre_slot.hip, default) / 0 rocPRIM and hipMemsetAsync (A/B)
     // kernel 5: capsule-chunk index, rebuilt per gather (bre_chunk.hip)
@@ -941,8 +943,8 @@ bre_status bre_set_option(bre_ctx *c, int option, int64_t value) {
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "readback mode must be 0 or 1");
         c->kernel_readback = (int)value;
         return BRE_OK;
-    case 121:  // internal: coarse sort keys (1, default: the tree-order sort on bits [16, 64), the segment
-               // sort on [12, 60): 6 radix passes each instead of 8) / all bits (0)
+    case 121:  // internal: coarse sort keys (1: the tree-order sort on bits [16, 64), the segment sort on
+               // [12, 60): 6 radix passes each instead of 8) / all bits (0, default)
         if (value < 0 || value > 1) return fail(c, BRE_ERR_INVALID_ARG, "coarse keys mode must be 0 or 1");
         c->coarse_keys = (int)value;
         return BRE_OK;

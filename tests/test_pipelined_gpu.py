@@ -132,7 +132,7 @@ def test_gather_events_bracket_the_tile_kernel(bre, scene_mod_gpu):
 
 
 def test_coarse_sort_keys_keep_every_pair(bre, scene_mod_gpu):
-    """Internal option 121 (default 1): the tree-order and segment sorts use the keys' top 48 bits.  Only
+    """Internal option 121 (1; default 0): the tree-order and segment sorts use the keys' top 48 bits.  Only
     orders change (the tree's leaf tiles, the packets), so every segment keeps its contribution count and
     its sum to float summation order, in camera-pass order."""
     import torch
